@@ -1,0 +1,126 @@
+/*
+ * icp_hip.h — C-ABI of libicp_hip.so, the MI355X (gfx950) device path of the ICP
+ * correspondence-and-alignment loop. Plain C types only; one context drives one GPU; several
+ * contexts (one process per GPU) cooperate through an RCCL communicator.
+ *
+ * Reference interfaces these entry points replace (B1AnKAlpha/IterativeClosestPoint):
+ *   icp_hip_set_target   Octree::Octree(const std::vector<Point3D>&, int max_pts, int max_d)
+ *                        PointCloudRegistration/core/octree.h:29, octree.cpp:41-126
+ *                        (CLI copy icp_registration.cpp:154-190)
+ *   icp_hip_nn           Octree::findNearest(const Point3D&) per query + residual
+ *                        octree.h:32, octree.cpp:175-184; icpengine.cpp:172-206
+ *   icp_hip_set_source   src/src3d packing, icpengine.cpp:139-152 (CLI :459-470)
+ *   icp_hip_iterate      one loop body of ICPEngine::runICP up to the SVD:
+ *                        icpengine.cpp:168-337 (NN, residuals, 3-sigma, cull, RMSE, centroids,
+ *                        cross-covariance), with the previous iteration's src = T*src
+ *                        (icpengine.cpp:345) fused in front. CLI twin: icp_registration.cpp:481-585
+ *   icp_hip_apply        src = T * src (icpengine.cpp:345-346; CLI :598-603)
+ *   icp_hip_get_source   write-back of the source (icpengine.cpp:371-375; CLI :609-613)
+ *   icp_hip_get_correspondences  `correspondences` vector (icpengine.cpp:169-179)
+ *
+ * Errors: every call returns ICP_HIP_OK (0) or a negative ICP_HIP_E* code; the message is in
+ * icp_hip_last_error() (thread-local). Host buffers are borrowed for the duration of a call.
+ * A context is driven by one host thread at a time.
+ */
+#ifndef ICP_HIP_H
+#define ICP_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ICP_HIP_OK 0
+#define ICP_HIP_EINVAL (-1)
+#define ICP_HIP_ENOMEM (-2)
+#define ICP_HIP_EDEVICE (-3)
+#define ICP_HIP_ERCCL (-4)
+#define ICP_HIP_ENOTREADY (-5)
+
+#define ICP_HIP_UNIQUE_ID_BYTES 128
+
+/* Which reference flavour an iteration follows (they differ in the octree's initial best
+ * distance and the first-iteration threshold). */
+#define ICP_RULES_ENGINE 0 /* core/icpengine.cpp: best = DBL_MAX, iter-0 relaxed threshold */
+#define ICP_RULES_CLI 1    /* icp_registration.cpp: best = 1e20, threshold mean + 3 std  */
+
+typedef struct icp_hip_ctx icp_hip_ctx;
+
+/* Statistics of one iteration, global over all ranks (identical on every rank). */
+typedef struct icp_iter_stats {
+  int64_t n;          /* source points (all ranks)                              */
+  double mean;        /* mean residual                       icpengine.cpp:235-239 */
+  double std;         /* population std of the residuals     icpengine.cpp:241-245 */
+  double threshold;   /* cull threshold                      icpengine.cpp:249-255 */
+  int64_t valid;      /* pairs with d <= threshold           icpengine.cpp:263-271 */
+  double rmse;        /* sqrt(sum_valid d^2 / valid)         icpengine.cpp:274-278 */
+  double sum_d2;
+  double min_d, max_d;/* over finite residuals               icpengine.cpp:220-223 */
+  int64_t n_bad;      /* non-finite residuals                icpengine.cpp:208-218 */
+  double centroid_src[3]; /* mean of valid source points     icpengine.cpp:82     */
+  double centroid_tgt[3]; /* mean of matched target points   icpengine.cpp:83     */
+  double H[9];        /* sum (a-ca)(b-cb)^T row-major        icpengine.cpp:86-90  */
+} icp_iter_stats;
+
+int icp_hip_device_count(int* count);
+
+/* Create a context on `device` (HIP ordinal). */
+int icp_hip_create(icp_hip_ctx** out, int device);
+void icp_hip_destroy(icp_hip_ctx* ctx);
+
+/* Multi-GPU: rank 0 calls get_unique_id, the caller distributes the bytes (any side channel),
+ * then every rank calls comm_init. Without it a context is a world of one. */
+int icp_hip_get_unique_id(uint8_t out[ICP_HIP_UNIQUE_ID_BYTES]);
+int icp_hip_comm_init(icp_hip_ctx* ctx, int nranks, int rank, const uint8_t id[ICP_HIP_UNIQUE_ID_BYTES]);
+
+/* Build the reference octree of the target (AoS xyz, n points) on the host and upload it.
+ * rules selects the initial best distance of findNearest. Non-finite target coordinates
+ * and empty targets are rejected (ICP_HIP_EINVAL). */
+int icp_hip_set_target(icp_hip_ctx* ctx, const double* xyz, int64_t n, int max_points, int max_depth,
+                       int rules);
+
+/* Upload this rank's source shard (AoS xyz). Queries are reordered on the device along a
+ * Morton curve for traversal coherence; every output is returned in the caller's order. */
+int icp_hip_set_source(icp_hip_ctx* ctx, const double* xyz, int64_t n);
+
+/* One ICP iteration body. If T_apply (row-major 4x4) is non-null, src = T_apply * src is applied
+ * first (fused into the search kernel). `iter` and `rules` select the threshold rule,
+ * sigma_multiplier is k in mean + k*std. Fills *out (identical on all ranks). */
+int icp_hip_iterate(icp_hip_ctx* ctx, const double* T_apply, int iter, int rules, double sigma_multiplier,
+                    icp_iter_stats* out);
+
+/* src = T * src on the resident source (row-major 4x4). */
+int icp_hip_apply(icp_hip_ctx* ctx, const double* T);
+
+/* Copy the resident (transformed) source back, AoS, caller's order. */
+int icp_hip_get_source(icp_hip_ctx* ctx, double* xyz_out);
+
+/* Correspondences (original target indices) and residuals of the last iterate, caller's order.
+ * Either pointer may be null. */
+int icp_hip_get_correspondences(icp_hip_ctx* ctx, int32_t* idx_out, double* dist_out);
+
+/* Parity hook: nearest target index + residual for arbitrary queries (AoS), no reordering,
+ * no transform — exactly Octree::findNearest + computeDistance per query. */
+int icp_hip_nn(icp_hip_ctx* ctx, const double* q_xyz, int64_t n, int32_t* idx_out, double* dist_out);
+
+/* Work of the reference DFS for the resident source (node entries and leaf points compared,
+ * both as the reference visits them) — the V and P of the roofline byte model. */
+int icp_hip_traversal_counts(icp_hip_ctx* ctx, double* mean_node_entries, double* mean_leaf_points);
+
+/* Shape of the uploaded octree. */
+int icp_hip_target_info(icp_hip_ctx* ctx, int64_t* n_nodes, int64_t* n_leaves, int32_t* max_depth,
+                        int32_t* stack_levels);
+
+/* Time (ms, HIP events on the context's stream) of the last search-kernel launch, and of the
+ * whole device part of the last iterate. */
+int icp_hip_last_timing(icp_hip_ctx* ctx, double* nn_kernel_ms, double* iterate_device_ms);
+
+int icp_hip_synchronize(icp_hip_ctx* ctx);
+
+const char* icp_hip_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

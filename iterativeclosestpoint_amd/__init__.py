@@ -1,0 +1,31 @@
+"""iterativeclosestpoint_amd — MI355X-native ICP correspondence-and-alignment path.
+
+The product is the C-ABI shared library ``libicp_hip.so`` (HIP kernels for gfx950 + C++ host
+driver, declared in ``include/icp_hip.h``, ``include/icp_engine.h``, ``include/icp_host.h``).
+This package is only the Python harness binding of that library (ctypes), used by the tests
+and ``bench.py``. There is no CPU fallback: if the library is missing the import of
+``lib()`` raises, and every device call fails loudly when no GPU is present.
+"""
+from ._lib import (  # noqa: F401
+    LIB_PATH,
+    IcpError,
+    Context,
+    lib,
+    build,
+    params_default,
+    engine_register,
+    cli_icp,
+    synth_pair,
+    octree_build,
+    jacobi_svd3,
+    best_fit_transform,
+    best_fit_from_stats,
+    moments_from_values,
+    moments_merge,
+    cov_from_pairs,
+    cov_merge,
+    cull_threshold,
+    RULES_ENGINE,
+    RULES_CLI,
+    FLAG_NO_EARLY_STOP,
+)

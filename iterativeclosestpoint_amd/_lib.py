@@ -1,0 +1,476 @@
+"""ctypes binding of libicp_hip.so (harness only; the product is the C-ABI library)."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+from pathlib import Path
+
+import numpy as np
+
+PKG_DIR = Path(__file__).resolve().parent
+REPO_DIR = PKG_DIR.parent
+LIB_PATH = PKG_DIR / "libicp_hip.so"
+
+RULES_ENGINE = 0
+RULES_CLI = 1
+FLAG_NO_EARLY_STOP = 1
+
+_P = C.c_void_p
+_D = C.POINTER(C.c_double)
+_I32 = C.POINTER(C.c_int32)
+
+
+class IcpError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"icp error {code}: {msg}")
+        self.code = code
+
+
+class IterStats(C.Structure):
+    _fields_ = [
+        ("n", C.c_int64), ("mean", C.c_double), ("std", C.c_double), ("threshold", C.c_double),
+        ("valid", C.c_int64), ("rmse", C.c_double), ("sum_d2", C.c_double), ("min_d", C.c_double),
+        ("max_d", C.c_double), ("n_bad", C.c_int64), ("centroid_src", C.c_double * 3),
+        ("centroid_tgt", C.c_double * 3), ("H", C.c_double * 9),
+    ]
+
+    def as_dict(self) -> dict:
+        out = {}
+        for name, _ in self._fields_:
+            v = getattr(self, name)
+            out[name] = list(v) if not isinstance(v, (int, float)) else v
+        return out
+
+
+class Params(C.Structure):
+    _fields_ = [
+        ("max_iterations", C.c_int32), ("tolerance", C.c_double), ("sigma_multiplier", C.c_double),
+        ("octree_max_points", C.c_int32), ("octree_max_depth", C.c_int32), ("rules", C.c_int32),
+        ("flags", C.c_int32),
+    ]
+
+
+class IterationRecord(C.Structure):
+    _fields_ = [
+        ("iteration", C.c_int32), ("rmse", C.c_double), ("valid_points", C.c_int32),
+        ("outlier_points", C.c_int32), ("transform", C.c_double * 16),
+        ("rotation_angle_deg", C.c_double), ("translation_distance", C.c_double),
+        ("has_transform", C.c_int32), ("mean", C.c_double), ("std", C.c_double),
+        ("threshold", C.c_double), ("increment", C.c_double * 16),
+    ]
+
+
+class Result(C.Structure):
+    _fields_ = [
+        ("success", C.c_int32), ("status", C.c_int32), ("total_iterations", C.c_int32),
+        ("final_rmse", C.c_double), ("final_R", C.c_double * 9), ("final_t", C.c_double * 3),
+        ("n_history", C.c_int32), ("message", C.c_char * 160),
+    ]
+
+
+ITER_CB = C.CFUNCTYPE(None, C.c_void_p, C.POINTER(IterationRecord))
+PROGRESS_CB = C.CFUNCTYPE(None, C.c_void_p, C.c_int, C.c_int, C.c_double)
+LOG_CB = C.CFUNCTYPE(None, C.c_void_p, C.c_char_p)
+
+
+class Hooks(C.Structure):
+    _fields_ = [
+        ("user", C.c_void_p), ("on_iteration", ITER_CB), ("on_progress", PROGRESS_CB),
+        ("on_log", LOG_CB), ("stop_flag", C.POINTER(C.c_int32)),
+    ]
+
+
+class OctreeInfo(C.Structure):
+    _fields_ = [
+        ("n_nodes", C.c_int64), ("n_leaves", C.c_int64), ("n_points", C.c_int64),
+        ("max_depth", C.c_int32), ("max_inner_depth", C.c_int32), ("pos_of_orig0", C.c_int32),
+    ]
+
+
+class SynthSpec(C.Structure):
+    _fields_ = [
+        ("sigma", C.c_double * 3), ("yaw_deg", C.c_double), ("pitch_deg", C.c_double),
+        ("roll_deg", C.c_double), ("t", C.c_double * 3), ("noise_sigma", C.c_double),
+        ("outlier_fraction", C.c_double), ("seed_target", C.c_uint64), ("seed_source", C.c_uint64),
+    ]
+
+
+# (name, restype, argtypes) for every exported symbol; also the list the ABI test checks
+SIGNATURES = {
+    # icp_hip.h
+    "icp_hip_device_count": (C.c_int, [C.POINTER(C.c_int)]),
+    "icp_hip_create": (C.c_int, [C.POINTER(C.c_void_p), C.c_int]),
+    "icp_hip_destroy": (None, [_P]),
+    "icp_hip_get_unique_id": (C.c_int, [C.c_char_p]),
+    "icp_hip_comm_init": (C.c_int, [_P, C.c_int, C.c_int, C.c_char_p]),
+    "icp_hip_set_target": (C.c_int, [_P, _P, C.c_int64, C.c_int, C.c_int, C.c_int]),
+    "icp_hip_set_source": (C.c_int, [_P, _P, C.c_int64]),
+    "icp_hip_iterate": (C.c_int, [_P, _P, C.c_int, C.c_int, C.c_double, C.POINTER(IterStats)]),
+    "icp_hip_apply": (C.c_int, [_P, _P]),
+    "icp_hip_get_source": (C.c_int, [_P, _P]),
+    "icp_hip_get_correspondences": (C.c_int, [_P, _P, _P]),
+    "icp_hip_nn": (C.c_int, [_P, _P, C.c_int64, _P, _P]),
+    "icp_hip_traversal_counts": (C.c_int, [_P, _D, _D]),
+    "icp_hip_target_info": (C.c_int, [_P, C.POINTER(C.c_int64), C.POINTER(C.c_int64), _I32, _I32]),
+    "icp_hip_last_timing": (C.c_int, [_P, _D, _D]),
+    "icp_hip_synchronize": (C.c_int, [_P]),
+    "icp_hip_last_error": (C.c_char_p, []),
+    # icp_engine.h
+    "icp_params_default": (None, [C.POINTER(Params)]),
+    "icp_engine_register": (C.c_int, [C.POINTER(Params), _P, C.c_int64, _P, C.c_int64, C.c_int,
+                                      C.POINTER(Result), C.POINTER(IterationRecord), C.c_int32,
+                                      C.POINTER(Hooks)]),
+    "icp_engine_run": (C.c_int, [_P, C.POINTER(Params), C.POINTER(Result), C.POINTER(IterationRecord),
+                                 C.c_int32, C.POINTER(Hooks)]),
+    "icp_session_create": (C.c_int, [_P, C.POINTER(Params), C.POINTER(Hooks), C.POINTER(C.c_void_p)]),
+    "icp_session_step": (C.c_int, [_P, C.POINTER(IterationRecord), _I32, _I32]),
+    "icp_session_finish": (C.c_int, [_P, C.POINTER(Result)]),
+    "icp_session_transform": (None, [_P, _P]),
+    "icp_session_destroy": (None, [_P]),
+    "icp_cli_icp": (C.c_int, [_P, C.c_int64, _P, C.c_int64, C.c_int, C.c_double, _P, _P, _P, C.c_int32,
+                              _I32, C.c_int]),
+    "icp_jacobi_svd3": (None, [_P, _P, _P, _P]),
+    "icp_best_fit_transform": (None, [_P, _P, C.c_int64, _P]),
+    "icp_best_fit_from_stats": (None, [C.POINTER(IterStats), _P]),
+    "icp_mat4_mul": (None, [_P, _P, _P]),
+    # icp_host.h
+    "icp_octree_build": (C.c_void_p, [_P, C.c_int64, C.c_int, C.c_int]),
+    "icp_octree_free": (None, [_P]),
+    "icp_octree_get_info": (None, [_P, C.POINTER(OctreeInfo)]),
+    "icp_octree_copy_nodes": (None, [_P, _P, _P, _P, _P]),
+    "icp_octree_copy_points": (None, [_P, _P, _P]),
+    "icp_moments_from_values": (None, [_P, C.c_int64, _P]),
+    "icp_moments_merge": (None, [_P, C.c_int32, _P]),
+    "icp_cov_from_pairs": (None, [_P, _P, _P, C.c_int64, C.c_double, _P]),
+    "icp_cov_merge": (None, [_P, C.c_int32, _P]),
+    "icp_cull_threshold": (C.c_double, [C.c_double, C.c_double, C.c_double, C.c_int, C.c_int]),
+    "icp_synth_default": (None, [C.POINTER(SynthSpec)]),
+    "icp_synth_pair": (C.c_int, [C.POINTER(SynthSpec), C.c_int64, C.c_int64, _P, _P, _P]),
+}
+
+_LIB = None
+
+
+def build(verbose: bool = False) -> None:
+    """Compile libicp_hip.so in-tree for gfx950 (hipcc; no GPU needed)."""
+    jobs = str(min(16, os.cpu_count() or 4))
+    r = subprocess.run(["make", "-j", jobs, "-C", str(PKG_DIR / "csrc")], capture_output=True, text=True)
+    if verbose or r.returncode != 0:
+        print(r.stdout[-4000:], r.stderr[-4000:])
+    if r.returncode != 0:
+        raise RuntimeError("building libicp_hip.so failed")
+
+
+def lib() -> C.CDLL:
+    """Load libicp_hip.so; raises if it is missing (there is no fallback path)."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not LIB_PATH.exists():
+        raise ImportError(f"{LIB_PATH} not built: run `make -C iterativeclosestpoint_amd/csrc` "
+                          "or __graft_entry__.build() (no CPU fallback exists)")
+    L = C.CDLL(str(LIB_PATH))
+    for name, (res, args) in SIGNATURES.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _LIB = L
+    return L
+
+
+def _ptr(a: np.ndarray | None):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+def _aos(a) -> np.ndarray:
+    a = np.ascontiguousarray(np.asarray(a, dtype=np.float64))
+    if a.ndim != 2 or a.shape[1] != 3:
+        raise ValueError("expected an (n, 3) float64 array")
+    return a
+
+
+def _check(rc: int) -> None:
+    if rc != 0:
+        raise IcpError(rc, lib().icp_hip_last_error().decode(errors="replace"))
+
+
+def params_default(**kw) -> Params:
+    p = Params()
+    lib().icp_params_default(C.byref(p))
+    for k, v in kw.items():
+        setattr(p, k, v)
+    return p
+
+
+class Context:
+    """One GPU context (icp_hip_ctx) — see include/icp_hip.h."""
+
+    def __init__(self, device: int = 0):
+        self._h = C.c_void_p()
+        _check(lib().icp_hip_create(C.byref(self._h), device))
+        self.n_src = 0
+
+    def close(self):
+        if self._h:
+            lib().icp_hip_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self):
+        return self._h
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = C.create_string_buffer(128)
+        _check(lib().icp_hip_get_unique_id(buf))
+        return buf.raw
+
+    def comm_init(self, nranks: int, rank: int, uid: bytes):
+        _check(lib().icp_hip_comm_init(self._h, nranks, rank, C.c_char_p(bytes(uid))))
+
+    def set_target(self, xyz, max_points=10, max_depth=20, rules=RULES_ENGINE):
+        xyz = _aos(xyz)
+        _check(lib().icp_hip_set_target(self._h, _ptr(xyz), xyz.shape[0], max_points, max_depth, rules))
+
+    def set_source(self, xyz):
+        xyz = _aos(xyz)
+        _check(lib().icp_hip_set_source(self._h, _ptr(xyz), xyz.shape[0]))
+        self.n_src = xyz.shape[0]
+
+    def iterate(self, T_apply=None, iteration=0, rules=RULES_ENGINE, sigma=3.0) -> IterStats:
+        st = IterStats()
+        T = None if T_apply is None else np.ascontiguousarray(T_apply, dtype=np.float64).reshape(16)
+        _check(lib().icp_hip_iterate(self._h, _ptr(T), iteration, rules, sigma, C.byref(st)))
+        return st
+
+    def apply(self, T):
+        T = np.ascontiguousarray(T, dtype=np.float64).reshape(16)
+        _check(lib().icp_hip_apply(self._h, _ptr(T)))
+
+    def get_source(self) -> np.ndarray:
+        out = np.empty((self.n_src, 3), np.float64)
+        _check(lib().icp_hip_get_source(self._h, _ptr(out)))
+        return out
+
+    def get_correspondences(self):
+        idx = np.empty(self.n_src, np.int32)
+        d = np.empty(self.n_src, np.float64)
+        _check(lib().icp_hip_get_correspondences(self._h, _ptr(idx), _ptr(d)))
+        return idx, d
+
+    def nn(self, q):
+        q = _aos(q)
+        idx = np.empty(q.shape[0], np.int32)
+        d = np.empty(q.shape[0], np.float64)
+        _check(lib().icp_hip_nn(self._h, _ptr(q), q.shape[0], _ptr(idx), _ptr(d)))
+        return idx, d
+
+    def traversal_counts(self):
+        a, b = C.c_double(), C.c_double()
+        _check(lib().icp_hip_traversal_counts(self._h, C.byref(a), C.byref(b)))
+        return a.value, b.value
+
+    def target_info(self):
+        nn_, nl = C.c_int64(), C.c_int64()
+        md, lv = C.c_int32(), C.c_int32()
+        _check(lib().icp_hip_target_info(self._h, C.byref(nn_), C.byref(nl), C.byref(md), C.byref(lv)))
+        return {"n_nodes": nn_.value, "n_leaves": nl.value, "max_depth": md.value, "stack_levels": lv.value}
+
+    def last_timing(self):
+        a, b = C.c_double(), C.c_double()
+        _check(lib().icp_hip_last_timing(self._h, C.byref(a), C.byref(b)))
+        return a.value, b.value
+
+    def synchronize(self):
+        _check(lib().icp_hip_synchronize(self._h))
+
+    def session(self, params: Params) -> "Session":
+        return Session(self, params)
+
+    def run(self, params: Params, history_cap: int = 1024):
+        res = Result()
+        hist = (IterationRecord * max(1, history_cap))()
+        rc = lib().icp_engine_run(self._h, C.byref(params), C.byref(res), hist, history_cap, None)
+        return rc, res, [hist[k] for k in range(res.n_history)]
+
+
+class Session:
+    """Steppable ICP loop on a context (icp_session_*): one step = one reference loop body."""
+
+    def __init__(self, ctx: Context, params: Params):
+        self._ctx = ctx  # keep alive
+        self._h = C.c_void_p()
+        _check(lib().icp_session_create(ctx.handle, C.byref(params), None, C.byref(self._h)))
+        self.done = False
+
+    def step(self):
+        rec = IterationRecord()
+        produced, done = C.c_int32(0), C.c_int32(0)
+        rc = lib().icp_session_step(self._h, C.byref(rec), C.byref(produced), C.byref(done))
+        self.done = bool(done.value)
+        _check(rc)
+        return rec if produced.value else None
+
+    def transform(self) -> np.ndarray:
+        T = np.empty(16)
+        lib().icp_session_transform(self._h, _ptr(T))
+        return T.reshape(4, 4)
+
+    def finish(self):
+        res = Result()
+        rc = lib().icp_session_finish(self._h, C.byref(res))
+        return rc, res
+
+    def close(self):
+        if self._h:
+            lib().icp_session_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def engine_register(params: Params, src, tgt, device: int = -1, history_cap: int = 1024, stop_flag=None,
+                    on_log=None):
+    """ICPEngine::registerPointClouds drop-in. Returns (rc, result, history, src_out)."""
+    src = _aos(src).copy()
+    tgt = _aos(tgt)
+    res = Result()
+    hist = (IterationRecord * max(1, history_cap))()
+    hooks = None
+    keep = []
+    if stop_flag is not None or on_log is not None:
+        hooks = Hooks()
+        if stop_flag is not None:
+            hooks.stop_flag = C.cast(C.addressof(stop_flag), C.POINTER(C.c_int32))
+        if on_log is not None:
+            cb = LOG_CB(lambda u, m: on_log(m.decode(errors="replace")))
+            keep.append(cb)
+            hooks.on_log = cb
+    rc = lib().icp_engine_register(C.byref(params), _ptr(src), src.shape[0], _ptr(tgt), tgt.shape[0], device,
+                                   C.byref(res), hist, history_cap, C.byref(hooks) if hooks else None)
+    return rc, res, [hist[k] for k in range(res.n_history)], src
+
+
+def cli_icp(src, tgt, max_iterations=20, tolerance=1e-2, device: int = -1):
+    """ICP() of icp_registration.cpp drop-in. Returns (R, t, transforms, src_out)."""
+    src = _aos(src).copy()
+    tgt = _aos(tgt)
+    R = np.zeros(9)
+    t = np.zeros(3)
+    cap = max(1, max_iterations)
+    tr = np.zeros((cap, 16))
+    n = C.c_int32()
+    _check(lib().icp_cli_icp(_ptr(src), src.shape[0], _ptr(tgt), tgt.shape[0], max_iterations, tolerance, _ptr(R),
+                             _ptr(t), _ptr(tr), cap, C.byref(n), device))
+    return R.reshape(3, 3), t, tr[: n.value].reshape(-1, 4, 4), src
+
+
+def synth_pair(n_tgt: int, n_src: int | None = None, **overrides):
+    spec = SynthSpec()
+    lib().icp_synth_default(C.byref(spec))
+    for k, v in overrides.items():
+        if k in ("sigma", "t"):
+            getattr(spec, k)[:] = list(v)
+        else:
+            setattr(spec, k, v)
+    n_src = n_tgt if n_src is None else n_src
+    tgt = np.empty((n_tgt, 3))
+    src = np.empty((n_src, 3))
+    T = np.empty(16)
+    _check(lib().icp_synth_pair(C.byref(spec), n_tgt, n_src, _ptr(tgt), _ptr(src), _ptr(T)))
+    return tgt, src, T.reshape(4, 4)
+
+
+def octree_build(xyz, max_points=10, max_depth=20) -> dict:
+    """Host linear-octree build (the exact arrays the device path uploads)."""
+    xyz = _aos(xyz)
+    h = lib().icp_octree_build(_ptr(xyz), xyz.shape[0], max_points, max_depth)
+    if not h:
+        raise IcpError(-1, lib().icp_hip_last_error().decode())
+    try:
+        info = OctreeInfo()
+        lib().icp_octree_get_info(h, C.byref(info))
+        nn_ = info.n_nodes
+        box = np.empty((nn_, 6))
+        first = np.empty(nn_, np.int32)
+        meta = np.empty(nn_, np.uint32)
+        depth = np.empty(nn_, np.int32)
+        lib().icp_octree_copy_nodes(h, _ptr(box), _ptr(first), _ptr(meta), _ptr(depth))
+        pts = np.empty((info.n_points, 3))
+        orig = np.empty(info.n_points, np.int32)
+        lib().icp_octree_copy_points(h, _ptr(pts), _ptr(orig))
+    finally:
+        lib().icp_octree_free(h)
+    return {"box": box, "first": first, "meta": meta, "depth": depth, "pts": pts, "orig": orig,
+            "n_leaves": info.n_leaves, "max_depth": info.max_depth, "max_inner_depth": info.max_inner_depth,
+            "pos_of_orig0": info.pos_of_orig0}
+
+
+def jacobi_svd3(H):
+    H = np.ascontiguousarray(H, np.float64).reshape(9)
+    U, S, V = np.empty(9), np.empty(3), np.empty(9)
+    lib().icp_jacobi_svd3(_ptr(H), _ptr(U), _ptr(S), _ptr(V))
+    return U.reshape(3, 3), S, V.reshape(3, 3)
+
+
+def best_fit_transform(a, b):
+    a, b = _aos(a), _aos(b)
+    T = np.empty(16)
+    lib().icp_best_fit_transform(_ptr(a), _ptr(b), a.shape[0], _ptr(T))
+    return T.reshape(4, 4)
+
+
+def best_fit_from_stats(st: IterStats):
+    T = np.empty(16)
+    lib().icp_best_fit_from_stats(C.byref(st), _ptr(T))
+    return T.reshape(4, 4)
+
+
+def moments_from_values(d):
+    d = np.ascontiguousarray(d, np.float64)
+    out = np.empty(8)
+    lib().icp_moments_from_values(_ptr(d), d.shape[0], _ptr(out))
+    return out
+
+
+def moments_merge(parts):
+    parts = np.ascontiguousarray(parts, np.float64).reshape(-1, 8)
+    out = np.empty(8)
+    lib().icp_moments_merge(_ptr(parts), parts.shape[0], _ptr(out))
+    return out
+
+
+def cov_from_pairs(a, b, d, thr):
+    a, b = _aos(a), _aos(b)
+    d = np.ascontiguousarray(d, np.float64)
+    out = np.empty(20)
+    lib().icp_cov_from_pairs(_ptr(a), _ptr(b), _ptr(d), d.shape[0], thr, _ptr(out))
+    return out
+
+
+def cov_merge(parts):
+    parts = np.ascontiguousarray(parts, np.float64).reshape(-1, 20)
+    out = np.empty(20)
+    lib().icp_cov_merge(_ptr(parts), parts.shape[0], _ptr(out))
+    return out
+
+
+def cull_threshold(mean, sd, k_sigma, iteration, engine_rules):
+    return lib().icp_cull_threshold(mean, sd, k_sigma, iteration, engine_rules)

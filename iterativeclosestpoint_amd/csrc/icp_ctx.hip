@@ -1,0 +1,471 @@
+// icp_ctx.hip — the C-ABI context of libicp_hip.so (include/icp_hip.h).
+//
+// One context = one GPU = one HIP stream. Everything that belongs to the path lives in HBM for
+// the whole registration: the linear octree (64-B node records), the leaf-ordered target
+// (32-B points), the Morton-ordered source shard as SoA x/y/z, per-query match position and
+// residual, block partials. Per iteration the host sees one 1 KB record (IterDev).
+// Multi-GPU: each rank holds its shard of the source and a replica of the octree; the two
+// per-iteration exchanges are RCCL all-gathers of one Moments / one CovMoments record, merged
+// on the device in rank order, so every rank computes bitwise-identical statistics.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cfloat>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/icp_hip.h"
+#include "icp_ctx_internal.h"
+#include "kernels.h"
+#include "octree_build.h"
+
+using namespace icp;
+
+namespace {
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                          \
+  do {                                                                                         \
+    hipError_t e_ = (expr);                                                                    \
+    if (e_ != hipSuccess)                                                                      \
+      return fail(e_ == hipErrorOutOfMemory ? ICP_HIP_ENOMEM : ICP_HIP_EDEVICE,                \
+                  std::string(#expr) + ": " + hipGetErrorString(e_));                          \
+  } while (0)
+
+#define RCCL_TRY(expr)                                                                         \
+  do {                                                                                         \
+    ncclResult_t r_ = (expr);                                                                  \
+    if (r_ != ncclSuccess) return fail(ICP_HIP_ERCCL, std::string(#expr) + ": " + ncclGetErrorString(r_)); \
+  } while (0)
+
+template <typename T>
+hipError_t dalloc(T** p, size_t count) {
+  *p = nullptr;
+  if (count == 0) count = 1;
+  return hipMalloc(reinterpret_cast<void**>(p), count * sizeof(T));
+}
+
+template <typename T>
+void dfree(T*& p) {
+  if (p) (void)hipFree(p);
+  p = nullptr;
+}
+
+}  // namespace
+
+void icp_ctx_set_error(const char* msg) { g_err = msg; }
+
+static void free_source(icp_hip_ctx* c) {
+  dfree(c->x);
+  dfree(c->y);
+  dfree(c->z);
+  dfree(c->perm);
+  dfree(c->pos);
+  dfree(c->dist);
+  dfree(c->mparts);
+  dfree(c->cparts);
+  c->n_src = 0;
+}
+
+static void free_target(icp_hip_ctx* c) {
+  dfree(c->nodes);
+  dfree(c->pts);
+  c->n_nodes = 0;
+  c->n_tgt = 0;
+}
+
+extern "C" {
+
+int icp_hip_device_count(int* count) {
+  HIP_TRY(hipGetDeviceCount(count));
+  return ICP_HIP_OK;
+}
+
+int icp_hip_create(icp_hip_ctx** out, int device) {
+  if (!out) return fail(ICP_HIP_EINVAL, "null out");
+  *out = nullptr;
+  int ndev = 0;
+  hipError_t e = hipGetDeviceCount(&ndev);
+  if (e != hipSuccess || ndev == 0)
+    return fail(ICP_HIP_EDEVICE, std::string("no HIP device available: ") + hipGetErrorString(e));
+  if (device < 0 || device >= ndev) return fail(ICP_HIP_EINVAL, "device ordinal out of range");
+  HIP_TRY(hipSetDevice(device));
+  icp_hip_ctx* c = new icp_hip_ctx();
+  c->device = device;
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return fail(ICP_HIP_EDEVICE, "hipStreamCreate failed");
+  }
+  for (hipEvent_t* ev : {&c->ev_it0, &c->ev_it1, &c->ev_nn0, &c->ev_nn1}) (void)hipEventCreate(ev);
+  if (dalloc(&c->it, 1) != hipSuccess || hipHostMalloc(reinterpret_cast<void**>(&c->h_it), sizeof(IterDev)) != hipSuccess ||
+      dalloc(&c->counters, 2) != hipSuccess || dalloc(&c->Tbuf, 16) != hipSuccess) {
+    icp_hip_destroy(c);
+    return fail(ICP_HIP_ENOMEM, "context allocation failed");
+  }
+  (void)hipMemset(c->it, 0, sizeof(IterDev));
+  *out = c;
+  return ICP_HIP_OK;
+}
+
+void icp_hip_destroy(icp_hip_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  (void)hipStreamSynchronize(c->stream);
+  free_source(c);
+  free_target(c);
+  dfree(c->it);
+  dfree(c->counters);
+  dfree(c->Tbuf);
+  dfree(c->gm);
+  dfree(c->gc);
+  if (c->h_it) (void)hipHostFree(c->h_it);
+  if (c->comm) (void)ncclCommDestroy(c->comm);
+  for (hipEvent_t ev : {c->ev_it0, c->ev_it1, c->ev_nn0, c->ev_nn1})
+    if (ev) (void)hipEventDestroy(ev);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+int icp_hip_get_unique_id(uint8_t out[ICP_HIP_UNIQUE_ID_BYTES]) {
+  static_assert(sizeof(ncclUniqueId) == ICP_HIP_UNIQUE_ID_BYTES, "unique id size");
+  ncclUniqueId id;
+  RCCL_TRY(ncclGetUniqueId(&id));
+  std::memcpy(out, &id, sizeof(id));
+  return ICP_HIP_OK;
+}
+
+int icp_hip_comm_init(icp_hip_ctx* c, int nranks, int rank, const uint8_t id_bytes[ICP_HIP_UNIQUE_ID_BYTES]) {
+  if (!c || nranks < 1 || rank < 0 || rank >= nranks) return fail(ICP_HIP_EINVAL, "bad comm arguments");
+  HIP_TRY(hipSetDevice(c->device));
+  if (c->comm) {
+    (void)ncclCommDestroy(c->comm);
+    c->comm = nullptr;
+  }
+  c->nranks = nranks;
+  c->rank = rank;
+  if (nranks == 1) return ICP_HIP_OK;
+  ncclUniqueId id;
+  std::memcpy(&id, id_bytes, sizeof(id));
+  RCCL_TRY(ncclCommInitRank(&c->comm, nranks, id, rank));
+  dfree(c->gm);
+  dfree(c->gc);
+  HIP_TRY(dalloc(&c->gm, (size_t)nranks));
+  HIP_TRY(dalloc(&c->gc, (size_t)nranks));
+  return ICP_HIP_OK;
+}
+
+int icp_hip_set_target(icp_hip_ctx* c, const double* xyz, int64_t n, int max_points, int max_depth, int rules) {
+  if (!c || (!xyz && n > 0)) return fail(ICP_HIP_EINVAL, "null argument");
+  if (n <= 0) return fail(ICP_HIP_EINVAL, "empty target cloud (icpengine.cpp:31-34 rejects it)");
+  if (max_depth < 0 || max_depth > 60) return fail(ICP_HIP_EINVAL, "max_depth out of range [0, 60]");
+  FlatOctree t;
+  const char* why = nullptr;
+  if (!build_flat_octree(xyz, n, max_points, max_depth, &t, &why)) return fail(ICP_HIP_EINVAL, why ? why : "bad target");
+  HIP_TRY(hipSetDevice(c->device));
+  free_target(c);
+  HIP_TRY(dalloc(&c->nodes, t.nodes.size()));
+  HIP_TRY(dalloc(&c->pts, t.pts.size()));
+  HIP_TRY(hipMemcpyAsync(c->nodes, t.nodes.data(), t.nodes.size() * sizeof(NodeRec), hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemcpyAsync(c->pts, t.pts.data(), t.pts.size() * sizeof(TgtPt), hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  c->n_nodes = (int64_t)t.nodes.size();
+  c->n_leaves = t.n_leaves;
+  c->n_tgt = n;
+  c->pos0 = t.pos_of_orig0;
+  c->max_depth = t.max_depth;
+  c->levels = t.max_inner_depth + 1 > 0 ? t.max_inner_depth + 1 : 1;
+  c->init_best = (rules == ICP_RULES_CLI) ? 1e20 : DBL_MAX;  // icp_registration.cpp:201 / octree.cpp:180
+  return ICP_HIP_OK;
+}
+
+int icp_hip_set_source(icp_hip_ctx* c, const double* xyz, int64_t n) {
+  if (!c || (!xyz && n > 0) || n < 0) return fail(ICP_HIP_EINVAL, "bad source arguments");
+  if (n > (int64_t)0x7fffffff) return fail(ICP_HIP_EINVAL, "source shard larger than INT32_MAX points");
+  HIP_TRY(hipSetDevice(c->device));
+  free_source(c);
+  c->n_src = n;
+  const int levels = c->levels > 0 ? c->levels : 20;
+  c->nb_nn = nn_num_blocks(n, levels);
+  c->nb_cull = cull_num_blocks(n);
+  HIP_TRY(dalloc(&c->x, n));
+  HIP_TRY(dalloc(&c->y, n));
+  HIP_TRY(dalloc(&c->z, n));
+  HIP_TRY(dalloc(&c->perm, n));
+  HIP_TRY(dalloc(&c->pos, n));
+  HIP_TRY(dalloc(&c->dist, n));
+  HIP_TRY(dalloc(&c->mparts, (size_t)(c->nb_nn + 2 * ((c->nb_nn + 255) / 256) + 4)));
+  HIP_TRY(dalloc(&c->cparts, (size_t)(c->nb_cull + 2 * ((c->nb_cull + 255) / 256) + 4)));
+  if (n == 0) return ICP_HIP_OK;
+  // Morton order over the source's own bounding box (host pass, then device keys + radix sort)
+  double lo[3] = {DBL_MAX, DBL_MAX, DBL_MAX}, hi[3] = {-DBL_MAX, -DBL_MAX, -DBL_MAX};
+  for (int64_t i = 0; i < n; i++)
+    for (int k = 0; k < 3; k++) {
+      const double v = xyz[3 * i + k];
+      if (std::isfinite(v)) {
+        lo[k] = v < lo[k] ? v : lo[k];
+        hi[k] = v > hi[k] ? v : hi[k];
+      }
+    }
+  double inv[3];
+  for (int k = 0; k < 3; k++) {
+    if (!(hi[k] >= lo[k])) lo[k] = hi[k] = 0.0;
+    const double ext = hi[k] - lo[k];
+    inv[k] = ext > 0.0 ? 1.0 / ext : 0.0;
+  }
+  double* aos = nullptr;
+  double *ux = nullptr, *uy = nullptr, *uz = nullptr;
+  uint64_t *keys = nullptr, *keys_sorted = nullptr;
+  int32_t* iota = nullptr;
+  void* temp = nullptr;
+  size_t temp_bytes = 0;
+  auto cleanup = [&]() {
+    dfree(aos); dfree(ux); dfree(uy); dfree(uz); dfree(keys); dfree(keys_sorted); dfree(iota);
+    if (temp) (void)hipFree(temp);
+  };
+  hipError_t e = hipSuccess;
+  if ((e = dalloc(&aos, 3 * (size_t)n)) != hipSuccess || (e = dalloc(&ux, n)) != hipSuccess ||
+      (e = dalloc(&uy, n)) != hipSuccess || (e = dalloc(&uz, n)) != hipSuccess ||
+      (e = dalloc(&keys, n)) != hipSuccess || (e = dalloc(&keys_sorted, n)) != hipSuccess ||
+      (e = dalloc(&iota, n)) != hipSuccess) {
+    cleanup();
+    return fail(ICP_HIP_ENOMEM, std::string("set_source allocation: ") + hipGetErrorString(e));
+  }
+  e = hipMemcpyAsync(aos, xyz, 3 * sizeof(double) * n, hipMemcpyHostToDevice, c->stream);
+  if (e == hipSuccess) e = launch_morton(aos, n, lo, inv, ux, uy, uz, keys, iota, c->stream);
+  if (e == hipSuccess) e = sort_pairs(nullptr, &temp_bytes, keys, keys_sorted, iota, c->perm, n, c->stream);
+  if (e == hipSuccess) e = hipMalloc(&temp, temp_bytes > 0 ? temp_bytes : 1);
+  if (e == hipSuccess) e = sort_pairs(temp, &temp_bytes, keys, keys_sorted, iota, c->perm, n, c->stream);
+  if (e == hipSuccess) e = launch_gather_soa(c->perm, ux, uy, uz, c->x, c->y, c->z, n, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  cleanup();
+  if (e != hipSuccess) return fail(ICP_HIP_EDEVICE, std::string("set_source: ") + hipGetErrorString(e));
+  c->have_results = false;
+  return ICP_HIP_OK;
+}
+
+int icp_hip_iterate(icp_hip_ctx* c, const double* T_apply, int iter, int rules, double sigma_multiplier,
+                    icp_iter_stats* out) {
+  if (!c || !out) return fail(ICP_HIP_EINVAL, "null argument");
+  if (!c->nodes) return fail(ICP_HIP_ENOTREADY, "target not set");
+  if (!c->x && c->n_src > 0) return fail(ICP_HIP_ENOTREADY, "source not set");
+  if (c->nranks > 1 && !c->comm) return fail(ICP_HIP_ENOTREADY, "communicator not initialised");
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  HIP_TRY(hipEventRecord(c->ev_it0, s));
+  NNLaunch a;
+  std::memset(&a, 0, sizeof(a));
+  a.nodes = c->nodes;
+  a.pts = c->pts;
+  a.x = c->x;
+  a.y = c->y;
+  a.z = c->z;
+  a.pos_out = c->pos;
+  a.dist_out = c->dist;
+  a.part = c->mparts;
+  a.counters = c->counters;
+  a.n = c->n_src;
+  a.n_nodes = (int32_t)c->n_nodes;
+  a.pos0 = c->pos0;
+  a.levels = c->levels;
+  a.init_best = c->init_best;
+  a.apply = T_apply ? 1 : 0;
+  if (T_apply)
+    for (int k = 0; k < 12; k++) a.T[k] = T_apply[k];
+  HIP_TRY(hipEventRecord(c->ev_nn0, s));
+  HIP_TRY(launch_nn(a, s));
+  HIP_TRY(hipEventRecord(c->ev_nn1, s));
+  HIP_TRY(launch_merge_moments(c->mparts, c->nb_nn, &c->it->m_local, s));
+  const bool multi = c->nranks > 1;
+  if (multi)
+    RCCL_TRY(ncclAllGather(&c->it->m_local, c->gm, sizeof(Moments) / sizeof(double), ncclDouble, c->comm, s));
+  HIP_TRY(launch_finalize_moments(multi ? c->gm : nullptr, multi ? c->nranks : 1, c->it, sigma_multiplier, iter,
+                                  rules == ICP_RULES_ENGINE ? 1 : 0, s));
+  CullLaunch cl;
+  cl.x = c->x;
+  cl.y = c->y;
+  cl.z = c->z;
+  cl.pos = c->pos;
+  cl.dist = c->dist;
+  cl.pts = c->pts;
+  cl.it = c->it;
+  cl.part = c->cparts;
+  cl.n = c->n_src;
+  HIP_TRY(launch_cull_cov(cl, s));
+  HIP_TRY(launch_merge_cov(c->cparts, c->nb_cull, &c->it->c_local, s));
+  if (multi)
+    RCCL_TRY(ncclAllGather(&c->it->c_local, c->gc, sizeof(CovMoments) / sizeof(double), ncclDouble, c->comm, s));
+  HIP_TRY(launch_finalize_cov(multi ? c->gc : nullptr, multi ? c->nranks : 1, c->it, s));
+  HIP_TRY(hipMemcpyAsync(c->h_it, c->it, sizeof(IterDev), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipEventRecord(c->ev_it1, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  const IterDev& h = *c->h_it;
+  out->n = (int64_t)h.m_global.n;
+  out->mean = h.mean;
+  out->std = h.sd;
+  out->threshold = h.thr;
+  out->valid = (int64_t)h.c_global.n;
+  out->rmse = h.rmse;
+  out->sum_d2 = h.c_global.sum_d2;
+  out->min_d = h.m_global.dmin;
+  out->max_d = h.m_global.dmax;
+  out->n_bad = (int64_t)h.m_global.nbad;
+  for (int k = 0; k < 3; k++) {
+    out->centroid_src[k] = h.c_global.ma[k];
+    out->centroid_tgt[k] = h.c_global.mb[k];
+  }
+  for (int k = 0; k < 9; k++) out->H[k] = h.c_global.c[k];
+  c->have_results = true;
+  return ICP_HIP_OK;
+}
+
+int icp_hip_apply(icp_hip_ctx* c, const double* T) {
+  if (!c || !T) return fail(ICP_HIP_EINVAL, "null argument");
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(launch_apply(T, c->x, c->y, c->z, c->n_src, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return ICP_HIP_OK;
+}
+
+int icp_hip_get_source(icp_hip_ctx* c, double* xyz_out) {
+  if (!c || (!xyz_out && c->n_src > 0)) return fail(ICP_HIP_EINVAL, "null argument");
+  if (c->n_src == 0) return ICP_HIP_OK;
+  HIP_TRY(hipSetDevice(c->device));
+  double* aos = nullptr;
+  HIP_TRY(dalloc(&aos, 3 * (size_t)c->n_src));
+  hipError_t e = launch_scatter_aos(c->perm, c->x, c->y, c->z, aos, c->n_src, c->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(xyz_out, aos, 3 * sizeof(double) * c->n_src, hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  dfree(aos);
+  if (e != hipSuccess) return fail(ICP_HIP_EDEVICE, std::string("get_source: ") + hipGetErrorString(e));
+  return ICP_HIP_OK;
+}
+
+int icp_hip_get_correspondences(icp_hip_ctx* c, int32_t* idx_out, double* dist_out) {
+  if (!c) return fail(ICP_HIP_EINVAL, "null argument");
+  if (!c->have_results) return fail(ICP_HIP_ENOTREADY, "no iteration has run on this source");
+  if (c->n_src == 0) return ICP_HIP_OK;
+  HIP_TRY(hipSetDevice(c->device));
+  int32_t* di = nullptr;
+  double* dd = nullptr;
+  hipError_t e = hipSuccess;
+  if (idx_out) e = dalloc(&di, c->n_src);
+  if (e == hipSuccess && dist_out) e = dalloc(&dd, c->n_src);
+  if (e == hipSuccess) e = launch_scatter_corr(c->perm, c->pos, c->pts, di, c->dist, dd, c->n_src, c->stream);
+  if (e == hipSuccess && idx_out) e = hipMemcpyAsync(idx_out, di, sizeof(int32_t) * c->n_src, hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess && dist_out) e = hipMemcpyAsync(dist_out, dd, sizeof(double) * c->n_src, hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  dfree(di);
+  dfree(dd);
+  if (e != hipSuccess) return fail(ICP_HIP_EDEVICE, std::string("get_correspondences: ") + hipGetErrorString(e));
+  return ICP_HIP_OK;
+}
+
+int icp_hip_nn(icp_hip_ctx* c, const double* q, int64_t n, int32_t* idx_out, double* dist_out) {
+  if (!c || n < 0 || (n > 0 && !q)) return fail(ICP_HIP_EINVAL, "bad arguments");
+  if (!c->nodes) return fail(ICP_HIP_ENOTREADY, "target not set");
+  if (n == 0) return ICP_HIP_OK;
+  if (n > (int64_t)0x7fffffff) return fail(ICP_HIP_EINVAL, "too many queries");
+  HIP_TRY(hipSetDevice(c->device));
+  double *aos = nullptr, *x = nullptr, *y = nullptr, *z = nullptr, *d = nullptr, *dd = nullptr;
+  int32_t *pos = nullptr, *di = nullptr;
+  hipError_t e = hipSuccess;
+  if ((e = dalloc(&aos, 3 * (size_t)n)) == hipSuccess && (e = dalloc(&x, n)) == hipSuccess &&
+      (e = dalloc(&y, n)) == hipSuccess && (e = dalloc(&z, n)) == hipSuccess && (e = dalloc(&d, n)) == hipSuccess &&
+      (e = dalloc(&dd, n)) == hipSuccess && (e = dalloc(&pos, n)) == hipSuccess && (e = dalloc(&di, n)) == hipSuccess) {
+    e = hipMemcpyAsync(aos, q, 3 * sizeof(double) * n, hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) e = launch_deinterleave(aos, x, y, z, n, c->stream);
+    NNLaunch a;
+    std::memset(&a, 0, sizeof(a));
+    a.nodes = c->nodes;
+    a.pts = c->pts;
+    a.x = x;
+    a.y = y;
+    a.z = z;
+    a.pos_out = pos;
+    a.dist_out = d;
+    a.part = nullptr;
+    a.n = n;
+    a.n_nodes = (int32_t)c->n_nodes;
+    a.pos0 = c->pos0;
+    a.levels = c->levels;
+    a.init_best = c->init_best;
+    if (e == hipSuccess) e = launch_nn(a, c->stream);
+    if (e == hipSuccess) e = launch_scatter_corr(nullptr, pos, c->pts, di, d, dd, n, c->stream);
+    if (e == hipSuccess && idx_out) e = hipMemcpyAsync(idx_out, di, sizeof(int32_t) * n, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess && dist_out) e = hipMemcpyAsync(dist_out, dd, sizeof(double) * n, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  }
+  dfree(aos); dfree(x); dfree(y); dfree(z); dfree(d); dfree(dd); dfree(pos); dfree(di);
+  if (e != hipSuccess) return fail(e == hipErrorOutOfMemory ? ICP_HIP_ENOMEM : ICP_HIP_EDEVICE, std::string("nn: ") + hipGetErrorString(e));
+  return ICP_HIP_OK;
+}
+
+int icp_hip_traversal_counts(icp_hip_ctx* c, double* mean_entries, double* mean_points) {
+  if (!c || !mean_entries || !mean_points) return fail(ICP_HIP_EINVAL, "null argument");
+  if (!c->nodes || (!c->x && c->n_src > 0)) return fail(ICP_HIP_ENOTREADY, "target/source not set");
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipMemsetAsync(c->counters, 0, 2 * sizeof(unsigned long long), c->stream));
+  NNLaunch a;
+  std::memset(&a, 0, sizeof(a));
+  a.nodes = c->nodes;
+  a.pts = c->pts;
+  a.x = c->x;
+  a.y = c->y;
+  a.z = c->z;
+  a.pos_out = c->pos;  // same queries as the last iterate: identical outputs are rewritten
+  a.dist_out = c->dist;
+  a.part = nullptr;
+  a.counters = c->counters;
+  a.n = c->n_src;
+  a.n_nodes = (int32_t)c->n_nodes;
+  a.pos0 = c->pos0;
+  a.levels = c->levels;
+  a.init_best = c->init_best;
+  a.count = 1;
+  HIP_TRY(launch_nn(a, c->stream));
+  unsigned long long h[2] = {0, 0};
+  HIP_TRY(hipMemcpyAsync(h, c->counters, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  const double n = c->n_src > 0 ? (double)c->n_src : 1.0;
+  *mean_entries = (double)h[0] / n;
+  *mean_points = (double)h[1] / n;
+  return ICP_HIP_OK;
+}
+
+int icp_hip_target_info(icp_hip_ctx* c, int64_t* n_nodes, int64_t* n_leaves, int32_t* max_depth, int32_t* levels) {
+  if (!c) return fail(ICP_HIP_EINVAL, "null ctx");
+  if (n_nodes) *n_nodes = c->n_nodes;
+  if (n_leaves) *n_leaves = c->n_leaves;
+  if (max_depth) *max_depth = c->max_depth;
+  if (levels) *levels = c->levels;
+  return ICP_HIP_OK;
+}
+
+int icp_hip_last_timing(icp_hip_ctx* c, double* nn_ms, double* it_ms) {
+  if (!c) return fail(ICP_HIP_EINVAL, "null ctx");
+  HIP_TRY(hipSetDevice(c->device));
+  float a = 0.f, b = 0.f;
+  HIP_TRY(hipEventElapsedTime(&a, c->ev_nn0, c->ev_nn1));
+  HIP_TRY(hipEventElapsedTime(&b, c->ev_it0, c->ev_it1));
+  if (nn_ms) *nn_ms = a;
+  if (it_ms) *it_ms = b;
+  return ICP_HIP_OK;
+}
+
+int icp_hip_synchronize(icp_hip_ctx* c) {
+  if (!c) return fail(ICP_HIP_EINVAL, "null ctx");
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return ICP_HIP_OK;
+}
+
+const char* icp_hip_last_error(void) { return g_err.c_str(); }
+
+}  // extern "C"

@@ -1,0 +1,47 @@
+// icp_ctx_internal.h — layout of the C-ABI context (private to libicp_hip.so).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstdint>
+
+#include "kernels.h"
+
+struct icp_hip_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev_it0 = nullptr, ev_it1 = nullptr, ev_nn0 = nullptr, ev_nn1 = nullptr;
+
+  // target (replicated on every rank)
+  icp::NodeRec* nodes = nullptr;
+  icp::TgtPt* pts = nullptr;
+  int64_t n_nodes = 0, n_leaves = 0, n_tgt = 0;
+  int32_t pos0 = 0, max_depth = -1, levels = 1;
+  double init_best = 1.7976931348623157e308;
+
+  // this rank's source shard, Morton order (perm[k] = caller index of slot k)
+  int64_t n_src = 0;
+  double *x = nullptr, *y = nullptr, *z = nullptr;
+  int32_t* perm = nullptr;
+  int32_t* pos = nullptr;  // leaf-order position of the match
+  double* dist = nullptr;  // residual
+  icp::Moments* mparts = nullptr;
+  icp::CovMoments* cparts = nullptr;
+  int64_t nb_nn = 0, nb_cull = 0;
+  bool have_results = false;
+
+  // per-iteration record
+  icp::IterDev* it = nullptr;
+  icp::IterDev* h_it = nullptr;  // pinned
+  unsigned long long* counters = nullptr;
+  double* Tbuf = nullptr;
+
+  // multi-GPU
+  int nranks = 1, rank = 0;
+  ncclComm_t comm = nullptr;
+  icp::Moments* gm = nullptr;
+  icp::CovMoments* gc = nullptr;
+};
+
+void icp_ctx_set_error(const char* msg);

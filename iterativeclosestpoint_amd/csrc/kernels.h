@@ -1,0 +1,88 @@
+// kernels.h — launch wrappers of the gfx950 kernels (kernels.hip). Internal C++ API used by
+// the C-ABI context (icp_ctx.hip); no torch types anywhere.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "icp_common.h"
+
+namespace icp {
+
+// Device-resident per-iteration record. Written by the finalize kernels, read by the cull
+// kernel (threshold) and copied to the host once per iteration.
+struct IterDev {
+  Moments m_local;      // this rank's residual moments
+  Moments m_global;     // merged over ranks (rank order)
+  CovMoments c_local;   // this rank's valid-pair moments
+  CovMoments c_global;  // merged over ranks
+  double mean, sd, thr, rmse;
+  double pad[4];
+};
+
+struct NNLaunch {
+  const NodeRec* nodes;
+  const TgtPt* pts;
+  double* x;
+  double* y;
+  double* z;
+  int32_t* pos_out;
+  double* dist_out;
+  Moments* part;                   // one per block, may be null
+  unsigned long long* counters;    // [node entries, leaf points] (count mode only)
+  int64_t n;
+  int32_t n_nodes;
+  int32_t pos0;
+  int32_t levels;
+  double init_best;
+  double T[12];                    // row-major 3x4, used when apply != 0
+  int apply;
+  int count;
+};
+
+// Threads per block of the NN kernel for a given stack depth.
+int nn_block_threads(int levels);
+int64_t nn_num_blocks(int64_t n, int levels);
+hipError_t launch_nn(const NNLaunch& a, hipStream_t s);
+
+hipError_t launch_merge_moments(const Moments* part, int64_t nparts, Moments* out, hipStream_t s);
+// Merge `nranks` gathered moments (or `local` when gathered == null), compute mean/std/threshold.
+hipError_t launch_finalize_moments(const Moments* gathered, int nranks, IterDev* it, double k_sigma,
+                                   int iter, int engine_rules, hipStream_t s);
+
+struct CullLaunch {
+  const double* x;
+  const double* y;
+  const double* z;
+  const int32_t* pos;
+  const double* dist;
+  const TgtPt* pts;
+  const IterDev* it;
+  CovMoments* part;
+  int64_t n;
+};
+int64_t cull_num_blocks(int64_t n);
+hipError_t launch_cull_cov(const CullLaunch& a, hipStream_t s);
+hipError_t launch_merge_cov(const CovMoments* part, int64_t nparts, CovMoments* out, hipStream_t s);
+hipError_t launch_finalize_cov(const CovMoments* gathered, int nranks, IterDev* it, hipStream_t s);
+
+hipError_t launch_apply(const double T[12], double* x, double* y, double* z, int64_t n, hipStream_t s);
+
+// Setup helpers: AoS -> SoA + 63-bit Morton keys over [lo, lo + ext] (21 bits per axis).
+hipError_t launch_morton(const double* aos, int64_t n, const double lo[3], const double inv_ext[3],
+                         double* x, double* y, double* z, uint64_t* keys, int32_t* iota, hipStream_t s);
+hipError_t launch_gather_soa(const int32_t* perm, const double* xi, const double* yi, const double* zi,
+                             double* xo, double* yo, double* zo, int64_t n, hipStream_t s);
+hipError_t launch_scatter_aos(const int32_t* perm, const double* x, const double* y, const double* z,
+                              double* aos, int64_t n, hipStream_t s);
+hipError_t launch_scatter_corr(const int32_t* perm, const int32_t* pos, const TgtPt* pts,
+                               int32_t* idx_out, double* dist_in, double* dist_out, int64_t n,
+                               hipStream_t s);
+hipError_t launch_deinterleave(const double* aos, double* x, double* y, double* z, int64_t n, hipStream_t s);
+
+// Radix sort of (key, value) pairs via hipCUB; temp storage managed by the caller.
+hipError_t sort_pairs(void* temp, size_t* temp_bytes, const uint64_t* keys_in, uint64_t* keys_out,
+                      const int32_t* vals_in, int32_t* vals_out, int64_t n, hipStream_t s);
+
+}  // namespace icp

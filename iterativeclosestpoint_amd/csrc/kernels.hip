@@ -1,0 +1,616 @@
+// kernels.hip — gfx950 (CDNA4) kernels of the ICP correspondence-and-alignment path.
+//
+//  k_nn        one thread per source query: (optional) rigid transform of the query in place,
+//              exact depth-first octree search with a per-thread level stack in LDS, residual
+//              d = |q - t|, per-block residual moments (count, mean, M2, min, max, #non-finite).
+//              Reproduces Octree::searchNearest (core/octree.cpp:128-184) bit for bit: same
+//              box-distance arithmetic with its sqrt, same prune test m*m >= best, children
+//              visited in stable ascending-distance order, strict < in the leaf scan.
+//  k_cull_cov  3-sigma cull (icpengine.cpp:263-278) + valid-pair centroids and centered
+//              cross-covariance per block (icpengine.cpp:76-90), two passes over registers.
+//  k_merge_*   fixed-shape tree merges of block partials (Chan et al.), deterministic.
+//  k_finalize_* rank-ordered merge of the gathered per-rank partials, threshold, RMSE.
+//
+// Everything is fp64 and compiled with -ffp-contract=off: the reference is built without FMA.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include "kernels.h"
+
+namespace icp {
+
+namespace {
+
+constexpr int kWave = 64;
+
+__device__ __forceinline__ double box_dist(double lx, double ly, double lz, double hx, double hy,
+                                           double hz, double qx, double qy, double qz) {
+  // OctreeNode::minDistanceTo (octree.cpp:32-38)
+  const double dx = smax(0.0, smax(lx - qx, qx - hx));
+  const double dy = smax(0.0, smax(ly - qy, qy - hy));
+  const double dz = smax(0.0, smax(lz - qz, qz - hz));
+  return __builtin_sqrt(dx * dx + dy * dy + dz * dz);
+}
+
+template <int N>
+__device__ __forceinline__ void block_sum(double (&v)[N], double* red) {
+#pragma unroll
+  for (int off = kWave / 2; off >= 1; off >>= 1) {
+#pragma unroll
+    for (int k = 0; k < N; k++) v[k] += __shfl_xor(v[k], off, kWave);
+  }
+  const int w = threadIdx.x / kWave, lane = threadIdx.x % kWave, nw = blockDim.x / kWave;
+  if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < N; k++) red[w * N + k] = v[k];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < N; k++) {
+    double s = red[k];
+    for (int j = 1; j < nw; j++) s += red[j * N + k];
+    v[k] = s;
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ void block_minmax(double& mn, double& mx, double* red) {
+#pragma unroll
+  for (int off = kWave / 2; off >= 1; off >>= 1) {
+    const double a = __shfl_xor(mn, off, kWave);
+    const double b = __shfl_xor(mx, off, kWave);
+    mn = a < mn ? a : mn;
+    mx = b > mx ? b : mx;
+  }
+  const int w = threadIdx.x / kWave, lane = threadIdx.x % kWave, nw = blockDim.x / kWave;
+  if (lane == 0) {
+    red[2 * w] = mn;
+    red[2 * w + 1] = mx;
+  }
+  __syncthreads();
+  mn = red[0];
+  mx = red[1];
+  for (int j = 1; j < nw; j++) {
+    mn = red[2 * j] < mn ? red[2 * j] : mn;
+    mx = red[2 * j + 1] > mx ? red[2 * j + 1] : mx;
+  }
+  __syncthreads();
+}
+
+// Stack entry: bits 0..31 first child record, bits 32..55 up to 8 pending children as 3-bit
+// ranks inside the contiguous child block (next child in the low bits), bits 56..59 count.
+__device__ __forceinline__ uint64_t pack_entry(int32_t first, uint32_t ranks, uint32_t cnt) {
+  return ((uint64_t)(ranks | (cnt << 24)) << 32) | (uint32_t)first;
+}
+
+template <bool APPLY, bool COUNT>
+__global__ void __launch_bounds__(256) k_nn(NNLaunch a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned long long lds_stack[];
+  const int bs = blockDim.x;
+  const int64_t i = (int64_t)blockIdx.x * bs + threadIdx.x;
+  const bool active = i < a.n;
+
+  double qx = 0.0, qy = 0.0, qz = 0.0;
+  if (active) {
+    qx = a.x[i];
+    qy = a.y[i];
+    qz = a.z[i];
+    if (APPLY) {
+      // src = T * src, Eigen order ((T0 x + T1 y) + T2 z) + T3 (icpengine.cpp:345)
+      const double nx = ((a.T[0] * qx + a.T[1] * qy) + a.T[2] * qz) + a.T[3];
+      const double ny = ((a.T[4] * qx + a.T[5] * qy) + a.T[6] * qz) + a.T[7];
+      const double nz = ((a.T[8] * qx + a.T[9] * qy) + a.T[10] * qz) + a.T[11];
+      a.x[i] = nx;
+      a.y[i] = ny;
+      a.z[i] = nz;
+      qx = nx;
+      qy = ny;
+      qz = nz;
+    }
+  }
+
+  double best_d2 = a.init_best;
+  int32_t best = -1;
+  double visits = 0.0, scanned = 0.0;
+  // A NaN coordinate makes every leaf distance NaN, so the reference never updates best_idx
+  // (octree.cpp:146): skipping the search is exact. (Its box distances stay finite: max(0,NaN)=0.)
+  const bool nan_q = (qx != qx) || (qy != qy) || (qz != qz);
+  if (active && !nan_q && a.n_nodes > 0) {
+    unsigned long long* st = lds_stack + threadIdx.x;
+    int sp = 0;
+    int32_t node = 0;
+    bool siblings_on_top = false;
+    if (COUNT) visits += 1.0;
+    while (true) {
+      const NodeRec* r = a.nodes + node;
+      const double2 l01 = *reinterpret_cast<const double2*>(&r->lo[0]);
+      const double2 l2h0 = *reinterpret_cast<const double2*>(&r->lo[2]);
+      const double2 h12 = *reinterpret_cast<const double2*>(&r->hi[1]);
+      const int4 topo = *reinterpret_cast<const int4*>(&r->first);
+      const double lx = l01.x, ly = l01.y, lz = l2h0.x, hx = l2h0.y, hy = h12.x, hz = h12.y;
+      const double m = box_dist(lx, ly, lz, hx, hy, hz, qx, qy, qz);
+      const int32_t first = topo.x;
+      const uint32_t meta = (uint32_t)topo.y;
+      if (m * m >= best_d2) {
+        // Pruned (octree.cpp:134-135). Siblings still pending on the top level come later in
+        // ascending distance, so they would all be pruned too: drop the level (exact).
+        if (siblings_on_top) sp--;
+      } else if (meta & kLeafBit) {
+        const int32_t cnt = (int32_t)(meta & ~kLeafBit);
+        if (COUNT) scanned += (double)cnt;
+        for (int32_t k = 0; k < cnt; k++) {
+          const TgtPt* p = a.pts + first + k;
+          const double2 pxy = *reinterpret_cast<const double2*>(&p->x);
+          const double pz = p->z;
+          const double dx = pxy.x - qx;
+          const double dy = pxy.y - qy;
+          const double dz = pz - qz;
+          const double d2 = dx * dx + dy * dy + dz * dz;
+          if (d2 < best_d2) {  // strict <, ascending original index inside a leaf
+            best_d2 = d2;
+            best = first + k;
+          }
+        }
+      } else {
+        // Inner node: distances of the existing children from the parent box and its
+        // midpoint (the stored child boxes are exactly these values, octree.cpp:97-120).
+        const double mx = (lx + hx) / 2, my = (ly + hy) / 2, mz = (lz + hz) / 2;
+        const double ax0 = smax(0.0, smax(lx - qx, qx - mx)), ax1 = smax(0.0, smax(mx - qx, qx - hx));
+        const double ay0 = smax(0.0, smax(ly - qy, qy - my)), ay1 = smax(0.0, smax(my - qy, qy - hy));
+        const double az0 = smax(0.0, smax(lz - qz, qz - mz)), az1 = smax(0.0, smax(mz - qz, qz - hz));
+        const double sx[2] = {ax0 * ax0, ax1 * ax1};
+        const double sy[2] = {ay0 * ay0, ay1 * ay1};
+        const double sz[2] = {az0 * az0, az1 * az1};
+        const uint32_t mask = meta & 0xffu;
+        double cd[8];
+#pragma unroll
+        for (int o = 0; o < 8; o++) cd[o] = __builtin_sqrt(sx[o & 1] + sy[(o >> 1) & 1] + sz[o >> 2]);
+        // Stable order = sort by (distance, octant): rank = #children strictly before.
+        uint32_t rk[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+        for (int p = 0; p < 8; p++) {
+#pragma unroll
+          for (int q = p + 1; q < 8; q++) {
+            const bool both = ((mask >> p) & 1u) && ((mask >> q) & 1u);
+            const bool q_first = cd[q] < cd[p];
+            rk[p] += (both && q_first) ? 1u : 0u;
+            rk[q] += (both && !q_first) ? 1u : 0u;
+          }
+        }
+        uint32_t ranks = 0;
+#pragma unroll
+        for (int o = 0; o < 8; o++) {
+          if ((mask >> o) & 1u) {
+            const uint32_t block_slot = (uint32_t)__builtin_popcount(mask & ((1u << o) - 1u));
+            ranks |= block_slot << (3u * rk[o]);
+          }
+        }
+        const uint32_t nch = (uint32_t)__builtin_popcount(mask);
+        if (COUNT) visits += (double)nch;
+        node = first + (int32_t)(ranks & 7u);
+        if (nch > 1) {
+          st[sp * bs] = pack_entry(first, ranks >> 3, nch - 1);
+          sp++;
+          siblings_on_top = true;
+        } else {
+          siblings_on_top = false;
+        }
+        continue;
+      }
+      if (sp == 0) break;
+      const unsigned long long e = st[(sp - 1) * bs];
+      const int32_t base = (int32_t)(uint32_t)e;
+      const uint32_t hi = (uint32_t)(e >> 32);
+      const uint32_t rem = (hi >> 24) - 1u;
+      node = base + (int32_t)(hi & 7u);
+      if (rem == 0) {
+        sp--;
+        siblings_on_top = false;
+      } else {
+        st[(sp - 1) * bs] = pack_entry(base, (hi & 0xffffffu) >> 3, rem);
+        siblings_on_top = true;
+      }
+    }
+  }
+
+  int32_t pos = best;
+  double d = 0.0;
+  if (active) {
+    if (best >= 0) {
+      d = __builtin_sqrt(best_d2);  // == computeDistance(src, tgt) bit for bit
+    } else {
+      // findNearest returned its default index 0 (octree.cpp:179); distance to that point.
+      pos = a.pos0;
+      const TgtPt p = a.pts[pos];
+      const double dx = qx - p.x, dy = qy - p.y, dz = qz - p.z;
+      d = __builtin_sqrt(dx * dx + dy * dy + dz * dz);
+    }
+    a.pos_out[i] = pos;
+    a.dist_out[i] = d;
+  }
+
+  __syncthreads();  // every traversal is done: reuse the stack LDS for the reductions
+  double* red = reinterpret_cast<double*>(lds_stack);
+  if (a.part) {
+    double s1[2] = {active ? 1.0 : 0.0, active ? d : 0.0};
+    block_sum<2>(s1, red);
+    const double nb = s1[0];
+    const double mean = s1[1] / nb;
+    const double dev = active ? (d - mean) : 0.0;
+    const bool fin = active && __builtin_isfinite(d);
+    double s2[2] = {dev * dev, (active && !fin) ? 1.0 : 0.0};
+    block_sum<2>(s2, red);
+    double mn = fin ? d : 1.7976931348623157e308, mxv = fin ? d : 0.0;
+    block_minmax(mn, mxv, red);
+    if (threadIdx.x == 0) {
+      Moments m;
+      m.n = nb;
+      m.mean = mean;
+      m.m2 = s2[0];
+      m.dmin = mn;
+      m.dmax = mxv;
+      m.nbad = s2[1];
+      m.pad0 = 0.0;
+      m.pad1 = 0.0;
+      a.part[blockIdx.x] = m;
+    }
+  }
+  if (COUNT) {
+    double c[2] = {visits, scanned};
+    block_sum<2>(c, red);
+    if (threadIdx.x == 0) {
+      atomicAdd(&a.counters[0], (unsigned long long)c[0]);
+      atomicAdd(&a.counters[1], (unsigned long long)c[1]);
+    }
+  }
+}
+
+// Fixed-shape tree merge: block b merges parts [256 b, 256 b + 256) pairwise in LDS.
+template <typename T, T (*Merge)(const T&, const T&), T (*Identity)()>
+__global__ void __launch_bounds__(256) k_tree_merge(const T* in, int64_t n, T* out) {
+  __shared__ T sm[256];
+  const int t = threadIdx.x;
+  const int64_t g = (int64_t)blockIdx.x * 256 + t;
+  sm[t] = (g < n) ? in[g] : Identity();
+  __syncthreads();
+  for (int s = 1; s < 256; s <<= 1) {
+    if ((t & (2 * s - 1)) == 0) sm[t] = Merge(sm[t], sm[t + s]);
+    __syncthreads();
+  }
+  if (t == 0) out[blockIdx.x] = sm[0];
+}
+
+__device__ Moments d_moments_merge(const Moments& a, const Moments& b) { return moments_merge(a, b); }
+__device__ Moments d_moments_identity() { return moments_identity(); }
+__device__ CovMoments d_cov_merge(const CovMoments& a, const CovMoments& b) { return cov_merge(a, b); }
+__device__ CovMoments d_cov_identity() { return cov_identity(); }
+
+__global__ void k_finalize_moments(const Moments* gathered, int nranks, IterDev* it, double k_sigma,
+                                   int iter, int engine_rules) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  Moments g = gathered ? gathered[0] : it->m_local;
+  for (int r = 1; r < nranks; r++) g = moments_merge(g, gathered[r]);
+  it->m_global = g;
+  // mean = sum/row; std = sqrt(variance/row) (icpengine.cpp:235-245)
+  const double mean = g.mean;
+  const double sd = __builtin_sqrt(g.m2 / g.n);
+  it->mean = mean;
+  it->sd = sd;
+  it->thr = cull_threshold(mean, sd, k_sigma, iter, engine_rules);
+}
+
+__global__ void __launch_bounds__(256) k_cull_cov(CullLaunch a) {
+  __shared__ double red[4 * 9];
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const double thr = a.it->thr;
+  bool valid = false;
+  double d = 0.0, ax = 0.0, ay = 0.0, az = 0.0, bx = 0.0, by = 0.0, bz = 0.0;
+  if (i < a.n) {
+    d = a.dist[i];
+    valid = d <= thr;  // icpengine.cpp:265
+    if (valid) {
+      ax = a.x[i];
+      ay = a.y[i];
+      az = a.z[i];
+      const TgtPt* p = a.pts + a.pos[i];
+      const double2 pxy = *reinterpret_cast<const double2*>(&p->x);
+      bx = pxy.x;
+      by = pxy.y;
+      bz = p->z;
+    }
+  }
+  double s1[8] = {valid ? 1.0 : 0.0, valid ? d * d : 0.0, ax, ay, az, bx, by, bz};
+  block_sum<8>(s1, red);
+  const double nb = s1[0];
+  if (nb == 0.0) {
+    if (threadIdx.x == 0) a.part[blockIdx.x] = cov_identity();
+    return;
+  }
+  const double ma[3] = {s1[2] / nb, s1[3] / nb, s1[4] / nb};
+  const double mb[3] = {s1[5] / nb, s1[6] / nb, s1[7] / nb};
+  const double ca[3] = {valid ? ax - ma[0] : 0.0, valid ? ay - ma[1] : 0.0, valid ? az - ma[2] : 0.0};
+  const double cb[3] = {valid ? bx - mb[0] : 0.0, valid ? by - mb[1] : 0.0, valid ? bz - mb[2] : 0.0};
+  double s2[9];
+#pragma unroll
+  for (int r = 0; r < 3; r++)
+#pragma unroll
+    for (int c = 0; c < 3; c++) s2[3 * r + c] = ca[r] * cb[c];
+  block_sum<9>(s2, red);
+  if (threadIdx.x == 0) {
+    CovMoments m;
+    m.n = nb;
+    m.sum_d2 = s1[1];
+    for (int k = 0; k < 3; k++) {
+      m.ma[k] = ma[k];
+      m.mb[k] = mb[k];
+    }
+    for (int k = 0; k < 9; k++) m.c[k] = s2[k];
+    m.pad[0] = 0.0;
+    m.pad[1] = 0.0;
+    m.pad[2] = 0.0;
+    a.part[blockIdx.x] = m;
+  }
+}
+
+__global__ void k_finalize_cov(const CovMoments* gathered, int nranks, IterDev* it) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  CovMoments g = gathered ? gathered[0] : it->c_local;
+  for (int r = 1; r < nranks; r++) g = cov_merge(g, gathered[r]);
+  it->c_global = g;
+  // rmse over valid pairs (icpengine.cpp:274-278)
+  it->rmse = (g.n > 0) ? __builtin_sqrt(g.sum_d2 / g.n) : 0.0;
+}
+
+__global__ void k_apply(const double* __restrict__ Tm, double* x, double* y, double* z, int64_t n) {
+  // T passed through a tiny device buffer to keep kernel args small
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const double qx = x[i], qy = y[i], qz = z[i];
+  x[i] = ((Tm[0] * qx + Tm[1] * qy) + Tm[2] * qz) + Tm[3];
+  y[i] = ((Tm[4] * qx + Tm[5] * qy) + Tm[6] * qz) + Tm[7];
+  z[i] = ((Tm[8] * qx + Tm[9] * qy) + Tm[10] * qz) + Tm[11];
+}
+
+struct T12 {
+  double v[12];
+};
+
+__global__ void k_apply_arg(T12 T, double* x, double* y, double* z, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const double qx = x[i], qy = y[i], qz = z[i];
+  x[i] = ((T.v[0] * qx + T.v[1] * qy) + T.v[2] * qz) + T.v[3];
+  y[i] = ((T.v[4] * qx + T.v[5] * qy) + T.v[6] * qz) + T.v[7];
+  z[i] = ((T.v[8] * qx + T.v[9] * qy) + T.v[10] * qz) + T.v[11];
+}
+
+__device__ __forceinline__ uint64_t spread3(uint64_t v) {
+  v &= 0x1fffff;
+  v = (v | (v << 32)) & 0x1f00000000ffffull;
+  v = (v | (v << 16)) & 0x1f0000ff0000ffull;
+  v = (v | (v << 8)) & 0x100f00f00f00f00full;
+  v = (v | (v << 4)) & 0x10c30c30c30c30c3ull;
+  v = (v | (v << 2)) & 0x1249249249249249ull;
+  return v;
+}
+
+__device__ __forceinline__ uint64_t quant21(double v, double lo, double inv) {
+  double f = (v - lo) * inv;
+  if (!(f > 0.0)) f = 0.0;  // also maps NaN to cell 0
+  if (f > 1.0) f = 1.0;
+  return (uint64_t)(f * 2097151.0);
+}
+
+struct Box {
+  double lo[3], inv[3];
+};
+
+__global__ void k_morton(const double* aos, int64_t n, Box b, double* x, double* y, double* z,
+                         uint64_t* keys, int32_t* iota) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const double px = aos[3 * i], py = aos[3 * i + 1], pz = aos[3 * i + 2];
+  x[i] = px;
+  y[i] = py;
+  z[i] = pz;
+  keys[i] = spread3(quant21(px, b.lo[0], b.inv[0])) | (spread3(quant21(py, b.lo[1], b.inv[1])) << 1) |
+            (spread3(quant21(pz, b.lo[2], b.inv[2])) << 2);
+  iota[i] = (int32_t)i;
+}
+
+__global__ void k_gather_soa(const int32_t* perm, const double* xi, const double* yi, const double* zi,
+                             double* xo, double* yo, double* zo, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int32_t j = perm[i];
+  xo[i] = xi[j];
+  yo[i] = yi[j];
+  zo[i] = zi[j];
+}
+
+__global__ void k_scatter_aos(const int32_t* perm, const double* x, const double* y, const double* z,
+                              double* aos, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t j = perm ? perm[i] : i;
+  aos[3 * j] = x[i];
+  aos[3 * j + 1] = y[i];
+  aos[3 * j + 2] = z[i];
+}
+
+__global__ void k_scatter_corr(const int32_t* perm, const int32_t* pos, const TgtPt* pts, int32_t* idx_out,
+                               const double* dist_in, double* dist_out, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t j = perm ? perm[i] : i;
+  if (idx_out) idx_out[j] = pts[pos[i]].orig;
+  if (dist_out) dist_out[j] = dist_in[i];
+}
+
+__global__ void k_deinterleave(const double* aos, double* x, double* y, double* z, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  x[i] = aos[3 * i];
+  y[i] = aos[3 * i + 1];
+  z[i] = aos[3 * i + 2];
+}
+
+inline unsigned grid_for(int64_t n, int bs) { return (unsigned)((n + bs - 1) / bs); }
+
+}  // namespace
+
+int nn_block_threads(int levels) {
+  // LDS stack: levels x threads x 8 B. Keep <= 64 KiB per block.
+  if (levels <= 32) return 256;
+  if (levels <= 64) return 128;
+  return 64;
+}
+
+int64_t nn_num_blocks(int64_t n, int levels) {
+  const int bs = nn_block_threads(levels);
+  return (n + bs - 1) / bs;
+}
+
+hipError_t launch_nn(const NNLaunch& a, hipStream_t s) {
+  if (a.n <= 0) return hipSuccess;
+  const int levels = a.levels < 1 ? 1 : a.levels;
+  const int bs = nn_block_threads(levels);
+  size_t shmem = (size_t)levels * bs * sizeof(unsigned long long);
+  if (shmem < 1024) shmem = 1024;  // also hosts the block reductions
+  const unsigned grid = grid_for(a.n, bs);
+  if (a.apply) {
+    if (a.count) hipLaunchKernelGGL((k_nn<true, true>), dim3(grid), dim3(bs), shmem, s, a);
+    else hipLaunchKernelGGL((k_nn<true, false>), dim3(grid), dim3(bs), shmem, s, a);
+  } else {
+    if (a.count) hipLaunchKernelGGL((k_nn<false, true>), dim3(grid), dim3(bs), shmem, s, a);
+    else hipLaunchKernelGGL((k_nn<false, false>), dim3(grid), dim3(bs), shmem, s, a);
+  }
+  return hipGetLastError();
+}
+
+static hipError_t tree_merge_moments(const Moments* in, int64_t n, Moments* scratch, Moments* out,
+                                     hipStream_t s) {
+  // in -> scratch (ceil(n/256)) -> ... -> out (1)
+  const Moments* cur = in;
+  int64_t cn = n;
+  Moments* bufs[2] = {scratch, scratch + ((n + 255) / 256)};
+  int k = 0;
+  while (cn > 256) {
+    const int64_t nb = (cn + 255) / 256;
+    hipLaunchKernelGGL((k_tree_merge<Moments, d_moments_merge, d_moments_identity>), dim3((unsigned)nb),
+                       dim3(256), 0, s, cur, cn, bufs[k]);
+    cur = bufs[k];
+    cn = nb;
+    k ^= 1;
+  }
+  hipLaunchKernelGGL((k_tree_merge<Moments, d_moments_merge, d_moments_identity>), dim3(1), dim3(256), 0, s,
+                     cur, cn, out);
+  return hipGetLastError();
+}
+
+static hipError_t tree_merge_cov(const CovMoments* in, int64_t n, CovMoments* scratch, CovMoments* out,
+                                 hipStream_t s) {
+  const CovMoments* cur = in;
+  int64_t cn = n;
+  CovMoments* bufs[2] = {scratch, scratch + ((n + 255) / 256)};
+  int k = 0;
+  while (cn > 256) {
+    const int64_t nb = (cn + 255) / 256;
+    hipLaunchKernelGGL((k_tree_merge<CovMoments, d_cov_merge, d_cov_identity>), dim3((unsigned)nb), dim3(256),
+                       0, s, cur, cn, bufs[k]);
+    cur = bufs[k];
+    cn = nb;
+    k ^= 1;
+  }
+  hipLaunchKernelGGL((k_tree_merge<CovMoments, d_cov_merge, d_cov_identity>), dim3(1), dim3(256), 0, s, cur,
+                     cn, out);
+  return hipGetLastError();
+}
+
+// The partial buffers are allocated with room for the merge scratch right behind the
+// block partials: parts[0 .. nparts) then 2 * ceil(nparts / 256) + 2 scratch entries.
+hipError_t launch_merge_moments(const Moments* part, int64_t nparts, Moments* out, hipStream_t s) {
+  Moments* scratch = const_cast<Moments*>(part) + nparts;
+  return tree_merge_moments(part, nparts, scratch, out, s);
+}
+
+hipError_t launch_merge_cov(const CovMoments* part, int64_t nparts, CovMoments* out, hipStream_t s) {
+  CovMoments* scratch = const_cast<CovMoments*>(part) + nparts;
+  return tree_merge_cov(part, nparts, scratch, out, s);
+}
+
+hipError_t launch_finalize_moments(const Moments* gathered, int nranks, IterDev* it, double k_sigma, int iter,
+                                   int engine_rules, hipStream_t s) {
+  hipLaunchKernelGGL(k_finalize_moments, dim3(1), dim3(64), 0, s, gathered, nranks, it, k_sigma, iter,
+                     engine_rules);
+  return hipGetLastError();
+}
+
+int64_t cull_num_blocks(int64_t n) { return (n + 255) / 256; }
+
+hipError_t launch_cull_cov(const CullLaunch& a, hipStream_t s) {
+  if (a.n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_cull_cov, dim3(grid_for(a.n, 256)), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_finalize_cov(const CovMoments* gathered, int nranks, IterDev* it, hipStream_t s) {
+  hipLaunchKernelGGL(k_finalize_cov, dim3(1), dim3(64), 0, s, gathered, nranks, it);
+  return hipGetLastError();
+}
+
+hipError_t launch_apply(const double T[12], double* x, double* y, double* z, int64_t n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  T12 t;
+  for (int k = 0; k < 12; k++) t.v[k] = T[k];
+  hipLaunchKernelGGL(k_apply_arg, dim3(grid_for(n, 256)), dim3(256), 0, s, t, x, y, z, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_morton(const double* aos, int64_t n, const double lo[3], const double inv_ext[3], double* x,
+                         double* y, double* z, uint64_t* keys, int32_t* iota, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  Box b;
+  for (int k = 0; k < 3; k++) {
+    b.lo[k] = lo[k];
+    b.inv[k] = inv_ext[k];
+  }
+  hipLaunchKernelGGL(k_morton, dim3(grid_for(n, 256)), dim3(256), 0, s, aos, n, b, x, y, z, keys, iota);
+  return hipGetLastError();
+}
+
+hipError_t launch_gather_soa(const int32_t* perm, const double* xi, const double* yi, const double* zi, double* xo,
+                             double* yo, double* zo, int64_t n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_gather_soa, dim3(grid_for(n, 256)), dim3(256), 0, s, perm, xi, yi, zi, xo, yo, zo, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_scatter_aos(const int32_t* perm, const double* x, const double* y, const double* z, double* aos,
+                              int64_t n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_scatter_aos, dim3(grid_for(n, 256)), dim3(256), 0, s, perm, x, y, z, aos, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_scatter_corr(const int32_t* perm, const int32_t* pos, const TgtPt* pts, int32_t* idx_out,
+                               double* dist_in, double* dist_out, int64_t n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_scatter_corr, dim3(grid_for(n, 256)), dim3(256), 0, s, perm, pos, pts, idx_out, dist_in,
+                     dist_out, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_deinterleave(const double* aos, double* x, double* y, double* z, int64_t n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_deinterleave, dim3(grid_for(n, 256)), dim3(256), 0, s, aos, x, y, z, n);
+  return hipGetLastError();
+}
+
+hipError_t sort_pairs(void* temp, size_t* temp_bytes, const uint64_t* keys_in, uint64_t* keys_out,
+                      const int32_t* vals_in, int32_t* vals_out, int64_t n, hipStream_t s) {
+  return hipcub::DeviceRadixSort::SortPairs(temp, *temp_bytes, keys_in, keys_out, vals_in, vals_out, (int)n, 0, 63,
+                                            s);
+}
+
+}  // namespace icp

@@ -1,0 +1,72 @@
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+GOLDEN = ROOT / "tests" / "golden"
+sys.path.insert(0, str(ROOT))
+sys.path.insert(0, str(ROOT / "oracle"))
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU; runs the HIP path")
+
+
+@pytest.fixture(scope="session")
+def golden_nn():
+    return np.load(GOLDEN / "nn_known_answers.npz")
+
+
+@pytest.fixture(scope="session")
+def golden_svd():
+    return np.load(GOLDEN / "svd_transform.npz")
+
+
+@pytest.fixture(scope="session")
+def golden_icp():
+    return np.load(GOLDEN / "icp_cli.npz")
+
+
+@pytest.fixture(scope="session")
+def golden_meta():
+    import json
+    return json.loads((GOLDEN / "golden.json").read_text())
+
+
+@pytest.fixture(scope="session")
+def icp():
+    import iterativeclosestpoint_amd as m
+    if not m.LIB_PATH.exists():
+        m.build()
+    m.lib()
+    return m
+
+
+@pytest.fixture(scope="session")
+def oracle():
+    import oracle_py
+    if not oracle_py.ORACLE_LIB.exists():
+        oracle_py.build(ref=False)
+    oracle_py.oracle()
+    return oracle_py
+
+
+@pytest.fixture(scope="session")
+def gpu_ctx(icp):
+    """One context on device 0 shared by the GPU tests (one process, as gpurun requires)."""
+    ctx = icp.Context(0)
+    yield ctx
+    ctx.close()
+
+
+def fnv1a(a: np.ndarray) -> str:
+    h = 0xCBF29CE484222325
+    for b in np.ascontiguousarray(a).tobytes():
+        h ^= b
+        h = (h * 0x100000001B3) & 0xFFFFFFFFFFFFFFFF
+    return f"{h:016x}"
+
+
+KAT_CASES = ["gauss", "lattice", "duplicates", "far", "single", "root_leaf"]

@@ -1,0 +1,195 @@
+#!/usr/bin/env python3
+"""Generate the golden fixtures under tests/golden/ from the REFERENCE ITSELF.
+
+The reference (B1AnKAlpha/IterativeClosestPoint) ships no tests, fixtures or golden data
+(SURVEY.md §4), so every vector here is produced in this container by the compiled
+reference: oracle/_ref/libicp_ref.so = /root/reference/icp_registration.cpp + its vendored
+Eigen 3.3.4, built by oracle/Makefile (`make -C oracle ref`). Inputs come from the product's
+deterministic generator (icp_synth_pair) or from numpy with fixed seeds, and are stored
+alongside (or as hashes, for the 100k case).
+
+Run from the repo root:  python tests/golden/gen_golden.py
+"""
+from __future__ import annotations
+
+import json
+import sys
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parents[2]
+sys.path.insert(0, str(ROOT))
+sys.path.insert(0, str(ROOT / "oracle"))
+
+import oracle_py as O  # noqa: E402
+import iterativeclosestpoint_amd as icp  # noqa: E402
+
+OUT = Path(__file__).resolve().parent
+
+
+def fnv1a(a: np.ndarray) -> str:
+    h = 0xCBF29CE484222325
+    for b in np.ascontiguousarray(a).tobytes():
+        h ^= b
+        h = (h * 0x100000001B3) & 0xFFFFFFFFFFFFFFFF
+    return f"{h:016x}"
+
+
+def nn_known_answers():
+    """(iii) NN known-answer sets: split planes, duplicates beyond leaf capacity, ties, far queries."""
+    rng = np.random.default_rng(7)
+    cases = {}
+    # a) Gaussian target, random + jittered-target queries
+    t = rng.normal(size=(8000, 3)) * [5, 5, 1]
+    q = np.concatenate([rng.normal(size=(3000, 3)) * [6, 6, 1.5], t[:1000] + rng.normal(size=(1000, 3)) * 1e-3])
+    cases["gauss"] = (t, q)
+    # b) integer lattice: many exact ties and points on split planes
+    g = np.stack(np.meshgrid(np.arange(12), np.arange(12), np.arange(6), indexing="ij"), -1).reshape(-1, 3).astype(float)
+    q = np.concatenate([g[rng.integers(0, len(g), 500)] + 0.5, rng.integers(-1, 13, size=(500, 3)).astype(float),
+                        g[rng.integers(0, len(g), 200)]])
+    cases["lattice"] = (g, q)
+    # c) heavy duplicates: 300 copies of a few points force leaves at max depth (> max_pts)
+    base = rng.normal(size=(5, 3))
+    dup = np.concatenate([np.repeat(base, 300, axis=0), rng.normal(size=(2000, 3)) * 3])
+    q = np.concatenate([base + 1e-9, rng.normal(size=(1000, 3)) * 3])
+    cases["duplicates"] = (dup, q)
+    # d) far-away queries (> 1e10): the CLI's 1e20 initial best (icp_registration.cpp:201) keeps
+    #    index 0 where the engine's DBL_MAX (octree.cpp:180) finds the true nearest
+    t = rng.normal(size=(2000, 3))
+    q = np.concatenate([rng.normal(size=(50, 3)) * 1e11, rng.normal(size=(50, 3))])
+    cases["far"] = (t, q)
+    # e) tiny targets: single point, root leaf (<= 10 points)
+    t = rng.normal(size=(1, 3))
+    cases["single"] = (t, rng.normal(size=(20, 3)))
+    t = rng.normal(size=(7, 3))
+    cases["root_leaf"] = (t, rng.normal(size=(50, 3)))
+    arrays = {}
+    meta = {}
+    for name, (t, q) in cases.items():
+        t = np.ascontiguousarray(t, np.float64)
+        q = np.ascontiguousarray(q, np.float64)
+        ref_idx = O.RefTree(t).nn(q)  # reference CLI octree, init 1e20, (10, 20)
+        arrays[f"{name}_target"] = t
+        arrays[f"{name}_query"] = q
+        arrays[f"{name}_idx_cli"] = ref_idx
+        # residual as the reference computes it: distance(src, target[idx]) (icp_registration.cpp:506)
+        d = np.array([O.reference().ref_distance(np.ascontiguousarray(q[i]).ctypes.data_as(O.C.c_void_p),
+                                                 np.ascontiguousarray(t[ref_idx[i]]).ctypes.data_as(O.C.c_void_p))
+                      for i in range(len(q))])
+        arrays[f"{name}_dist_cli"] = d
+        meta[name] = {"n_target": len(t), "n_query": len(q)}
+    # max_depth / max_points variants on the Gaussian set (the GUI range, settingspage.cpp:53-76)
+    t, q = cases["gauss"]
+    for mp, md in [(5, 10), (100, 50), (10, 3)]:
+        arrays[f"gauss_idx_cli_p{mp}_d{md}"] = O.RefTree(t, mp, md).nn(q)
+    np.savez_compressed(OUT / "nn_known_answers.npz", **arrays)
+    return meta
+
+
+def svd_and_transform():
+    rng = np.random.default_rng(11)
+    Hs = [rng.normal(size=(3, 3)) for _ in range(40)]
+    Hs += [np.diag(rng.normal(size=3)) for _ in range(4)]
+    Hs += [np.outer(rng.normal(size=3), rng.normal(size=3)) for _ in range(4)]  # rank 1
+    Hs += [np.zeros((3, 3)), np.eye(3), -np.eye(3), np.diag([1.0, 1.0, -1.0])]
+    Hs += [rng.normal(size=(3, 3)) * 1e8, rng.normal(size=(3, 3)) * 1e-8]
+    Hs = np.array(Hs)
+    fixed = [O.ref_svd3(H, False) for H in Hs]
+    dyn = [O.ref_svd3(H, True) for H in Hs]
+    # best_fit_transform on point sets (icp_registration.cpp:389-440)
+    A = [rng.normal(size=(n, 3)) * [5, 5, 1] + rng.normal(size=3) * 100 for n in (3, 10, 500, 5000)]
+    B = []
+    for a in A:
+        ang = rng.uniform(-0.2, 0.2)
+        R = np.array([[np.cos(ang), -np.sin(ang), 0], [np.sin(ang), np.cos(ang), 0], [0, 0, 1]])
+        B.append(a @ R.T + rng.normal(size=3) + rng.normal(size=a.shape) * 1e-3)
+    # reflection case: mirrored set
+    a = rng.normal(size=(50, 3))
+    A.append(a)
+    B.append(a * [1, 1, -1])
+    Tbf = [O.ref_best_fit(a, b) for a, b in zip(A, B)]
+    # Eigen T * src (4xN) and T * T_cum bits
+    T = np.eye(4)
+    T[:3, :3] = np.linalg.qr(rng.normal(size=(3, 3)))[0]
+    T[:3, 3] = rng.normal(size=3) * 10
+    pts = rng.normal(size=(4000, 3)) * [50, 50, 5] + [1e5, -2e5, 30]
+    tp = O.ref_transform(T, pts)
+    T2 = np.eye(4)
+    T2[:3, :3] = np.linalg.qr(rng.normal(size=(3, 3)))[0]
+    T2[:3, 3] = rng.normal(size=3)
+    mm = O.ref_mat4_mul(T, T2)
+    arrays = {
+        "H": Hs,
+        "U_fixed": np.array([f[0] for f in fixed]), "S_fixed": np.array([f[1] for f in fixed]),
+        "V_fixed": np.array([f[2] for f in fixed]),
+        "U_dyn": np.array([f[0] for f in dyn]), "S_dyn": np.array([f[1] for f in dyn]),
+        "V_dyn": np.array([f[2] for f in dyn]),
+        "T": T, "T2": T2, "pts": pts, "T_pts": tp, "T_T2": mm,
+        "T_bestfit": np.array(Tbf),
+    }
+    for k, (a, b) in enumerate(zip(A, B)):
+        arrays[f"bf_A{k}"] = a
+        arrays[f"bf_B{k}"] = b
+    np.savez_compressed(OUT / "svd_transform.npz", **arrays)
+    return {"n_H": len(Hs), "n_bestfit": len(A)}
+
+
+def icp_cli_cases():
+    """(i)/(ii): the reference CLI ICP() end to end on config-1 and 10k pairs."""
+    rng = np.random.default_rng(2024)
+    out = {}
+    arrays = {}
+    # config 1: test_icp.cpp-style random R (<= 10 deg) and t (+-2.5 m xy, +-1 m z) (test_icp.cpp:165-229)
+    angle = rng.uniform() * 10.0
+    yaw, pitch, roll = angle, (rng.uniform() - 0.5) * angle, (rng.uniform() - 0.5) * angle
+    t = [(rng.uniform() - 0.5) * 5, (rng.uniform() - 0.5) * 5, (rng.uniform() - 0.5) * 2]
+    specs = {
+        "cfg1_1k": dict(n=1000, yaw_deg=yaw, pitch_deg=pitch, roll_deg=roll, t=t, iters=20, tol=1e-2),
+        "g10k": dict(n=10000, yaw_deg=3.0, pitch_deg=1.0, roll_deg=-0.5, t=[0.3, -0.2, 0.05], iters=30, tol=1e-9),
+    }
+    for name, sp in specs.items():
+        tgt, src, Ttrue = icp.synth_pair(sp["n"], yaw_deg=sp["yaw_deg"], pitch_deg=sp["pitch_deg"],
+                                         roll_deg=sp["roll_deg"], t=sp["t"])
+        R, tt, tcums, src_out = O.ref_icp_cli(src, tgt, sp["iters"], sp["tol"])
+        idx0 = O.RefTree(tgt).nn(src)
+        arrays[f"{name}_target"] = tgt
+        arrays[f"{name}_source"] = src
+        arrays[f"{name}_T_true"] = Ttrue
+        arrays[f"{name}_R_final"] = R
+        arrays[f"{name}_t_final"] = tt
+        arrays[f"{name}_T_cums"] = tcums
+        arrays[f"{name}_source_out"] = src_out
+        arrays[f"{name}_idx_iter0"] = idx0
+        out[name] = {"n": sp["n"], "iterations": sp["iters"], "tolerance": sp["tol"],
+                     "n_transforms": int(len(tcums)), "synth": {k: v for k, v in sp.items() if k not in ("n",)}}
+    np.savez_compressed(OUT / "icp_cli.npz", **arrays)
+    return out
+
+
+def nn_100k_hashes():
+    """(ii) 100k Gaussian pair: inputs regenerated by icp_synth_pair; reference indices hashed."""
+    tgt, src, _ = icp.synth_pair(100000)
+    idx = O.RefTree(tgt).nn(src)
+    tree = O.OracleTree(tgt)
+    _, _, visits, scanned = tree.nn(src, count=True)
+    return {"n": 100000, "target_fnv1a": fnv1a(tgt), "source_fnv1a": fnv1a(src), "idx_fnv1a": fnv1a(idx),
+            "idx_sum": int(idx.astype(np.int64).sum()), "mean_node_entries": visits / len(src),
+            "mean_leaf_points": scanned / len(src)}
+
+
+def main():
+    if not O.reference_available():
+        O.build(ref=True)
+    meta = {"generator": "tests/golden/gen_golden.py", "reference": "icp_registration.cpp + vendored Eigen 3.3.4 "
+            "(oracle/_ref/libicp_ref.so, g++ -O2 -ffp-contract=off, no -march)"}
+    meta["nn_known_answers"] = nn_known_answers()
+    meta["svd_transform"] = svd_and_transform()
+    meta["icp_cli"] = icp_cli_cases()
+    meta["nn_100k"] = nn_100k_hashes()
+    (OUT / "golden.json").write_text(json.dumps(meta, indent=1, sort_keys=True))
+    print(json.dumps(meta, indent=1))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,46 @@
+"""The C-ABI library loads and exports every function declared in include/*.h (no GPU calls)."""
+import ctypes
+import re
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+DECL = re.compile(r"^[A-Za-z_][\w\s\*]*?\b(icp_\w+)\s*\(", re.M)
+
+
+def declared_functions():
+    names = set()
+    for h in sorted((ROOT / "include").glob("*.h")):
+        text = re.sub(r"/\*.*?\*/", "", h.read_text(), flags=re.S)
+        text = re.sub(r"//[^\n]*", "", text)
+        for m in DECL.finditer(text):
+            if not text[m.start():m.end()].lstrip().startswith(("typedef", "#")):
+                names.add(m.group(1))
+    return sorted(names)
+
+
+def test_headers_declare_functions():
+    names = declared_functions()
+    assert "icp_hip_iterate" in names and "icp_engine_register" in names and "icp_octree_build" in names
+    assert len(names) >= 30
+
+
+@pytest.mark.parametrize("name", declared_functions())
+def test_symbol_exported(icp, name):
+    lib = ctypes.CDLL(str(icp.LIB_PATH))
+    assert hasattr(lib, name), f"{name} declared in include/ but not exported"
+
+
+def test_binding_covers_headers(icp):
+    from iterativeclosestpoint_amd._lib import SIGNATURES
+    assert set(declared_functions()) <= set(SIGNATURES), set(declared_functions()) - set(SIGNATURES)
+
+
+def test_no_gpu_fails_loudly(icp):
+    """Without a GPU the device path refuses (no CPU fallback exists)."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    with pytest.raises(icp.IcpError):
+        icp.Context(0)

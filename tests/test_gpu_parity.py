@@ -1,0 +1,178 @@
+"""GPU parity tests: the HIP path through the C-ABI against the golden vectors of the reference
+and the CPU oracle on the same inputs.
+
+Bar (BASELINE.json north_star): correspondence indices bit-exact against the CPU octree for
+identical query coordinates (residuals too — they are sqrt of the same best distance);
+per-iteration statistics within 1e-12 relative (the GPU sums in a different order);
+final 4x4 transform within 1e-6 RMSE of the CPU/Eigen reference (observed ~1e-14).
+"""
+import numpy as np
+import pytest
+
+from conftest import KAT_CASES, fnv1a
+
+pytestmark = pytest.mark.gpu
+
+RMSE_TOL = 1e-6  # final transform, north_star
+
+
+def t_rmse(a, b):
+    return float(np.sqrt(np.mean((np.asarray(a) - np.asarray(b)) ** 2)))
+
+
+@pytest.mark.parametrize("case", KAT_CASES)
+def test_nn_kat_cli_rules(icp, gpu_ctx, golden_nn, case):
+    t, q = golden_nn[f"{case}_target"], golden_nn[f"{case}_query"]
+    gpu_ctx.set_target(t, 10, 20, icp.RULES_CLI)
+    idx, d = gpu_ctx.nn(q)
+    np.testing.assert_array_equal(idx, golden_nn[f"{case}_idx_cli"])
+    np.testing.assert_array_equal(d, golden_nn[f"{case}_dist_cli"])
+
+
+@pytest.mark.parametrize("case", KAT_CASES)
+def test_nn_kat_engine_rules(icp, oracle, gpu_ctx, golden_nn, case):
+    t, q = golden_nn[f"{case}_target"], golden_nn[f"{case}_query"]
+    gpu_ctx.set_target(t, 10, 20, icp.RULES_ENGINE)
+    idx, d = gpu_ctx.nn(q)
+    oidx, od = oracle.OracleTree(t).nn(q, init_best=oracle.DBL_MAX)
+    np.testing.assert_array_equal(idx, oidx)
+    np.testing.assert_array_equal(d, od)
+
+
+@pytest.mark.parametrize("mp,md", [(5, 10), (100, 50), (10, 3)])
+def test_nn_octree_params(icp, gpu_ctx, golden_nn, mp, md):
+    t, q = golden_nn["gauss_target"], golden_nn["gauss_query"]
+    gpu_ctx.set_target(t, mp, md, icp.RULES_CLI)
+    idx, _ = gpu_ctx.nn(q)
+    np.testing.assert_array_equal(idx, golden_nn[f"gauss_idx_cli_p{mp}_d{md}"])
+
+
+def test_nn_100k_reference_hash_and_work(icp, gpu_ctx, golden_meta):
+    m = golden_meta["nn_100k"]
+    tgt, src, _ = icp.synth_pair(m["n"])
+    gpu_ctx.set_target(tgt, 10, 20, icp.RULES_CLI)
+    idx, _ = gpu_ctx.nn(src)
+    assert fnv1a(idx) == m["idx_fnv1a"]
+    gpu_ctx.set_source(src)
+    gpu_ctx.iterate(None, 0, icp.RULES_CLI, 3.0)
+    v, p = gpu_ctx.traversal_counts()
+    # the kernel counts the reference DFS's node entries / scanned points exactly
+    assert v == pytest.approx(m["mean_node_entries"], rel=0, abs=1e-9)
+    assert p == pytest.approx(m["mean_leaf_points"], rel=0, abs=1e-9)
+
+
+def test_nn_edge_queries(icp, oracle, gpu_ctx):
+    rng = np.random.default_rng(5)
+    t = rng.normal(size=(3000, 3))
+    q = np.concatenate([
+        t[:50],                                   # exact hits
+        np.array([[np.nan, 0, 0], [0, np.inf, 0], [-np.inf, 1, 1], [np.nan] * 3]),
+        np.zeros((3, 3)), rng.normal(size=(50, 3)) * 100])
+    for rules, init in [(icp.RULES_ENGINE, oracle.DBL_MAX), (icp.RULES_CLI, 1e20)]:
+        gpu_ctx.set_target(t, 10, 20, rules)
+        idx, d = gpu_ctx.nn(q)
+        oidx, od = oracle.OracleTree(t).nn(q, init_best=init)
+        np.testing.assert_array_equal(idx, oidx)
+        np.testing.assert_array_equal(np.isnan(d), np.isnan(od))
+        np.testing.assert_array_equal(d[~np.isnan(d)], od[~np.isnan(od)])
+    np.testing.assert_array_equal(idx[:50], np.arange(50))
+
+
+def test_apply_bits_match_eigen(icp, gpu_ctx, golden_svd):
+    pts = golden_svd["pts"]
+    gpu_ctx.set_target(pts, 10, 20, icp.RULES_ENGINE)
+    gpu_ctx.set_source(pts)
+    gpu_ctx.apply(golden_svd["T"])
+    np.testing.assert_array_equal(gpu_ctx.get_source(), golden_svd["T_pts"])  # Eigen T*src bits
+
+
+def test_iterate_stats_match_oracle(icp, oracle, gpu_ctx):
+    tgt, src, _ = icp.synth_pair(20000, yaw_deg=4.0)
+    gpu_ctx.set_target(tgt, 10, 20, icp.RULES_ENGINE)
+    gpu_ctx.set_source(src)
+    st = gpu_ctx.iterate(None, 0, icp.RULES_ENGINE, 3.0)
+    oidx, od = oracle.OracleTree(tgt).nn(src, init_best=oracle.DBL_MAX)
+    idx, d = gpu_ctx.get_correspondences()
+    np.testing.assert_array_equal(idx, oidx)
+    np.testing.assert_array_equal(d, od)
+    mean = od.sum() / len(od)
+    sd = np.sqrt(((od - mean) ** 2).sum() / len(od))
+    thr = mean + max(3.0 * sd, 0.5 * mean)
+    v = od <= thr
+    assert st.n == len(src) and st.valid == int(v.sum())
+    np.testing.assert_allclose([st.mean, st.std, st.threshold], [mean, sd, thr], rtol=1e-12)
+    np.testing.assert_allclose(st.rmse, np.sqrt((od[v] ** 2).sum() / v.sum()), rtol=1e-12)
+    a, b = src[v], tgt[oidx[v]]
+    np.testing.assert_allclose(st.centroid_src, a.mean(0), rtol=1e-12, atol=1e-13)
+    np.testing.assert_allclose(st.centroid_tgt, b.mean(0), rtol=1e-12, atol=1e-13)
+    H = (a - a.mean(0)).T @ (b - b.mean(0))
+    np.testing.assert_allclose(np.array(st.H).reshape(3, 3), H, rtol=1e-10, atol=1e-10 * np.abs(H).max())
+    assert st.min_d == od.min() and st.max_d == od.max() and st.n_bad == 0
+    # host best fit from the device moments vs the oracle's (Eigen-equivalent) best fit
+    np.testing.assert_allclose(icp.best_fit_from_stats(st), oracle.best_fit(a, b), atol=1e-12)
+
+
+@pytest.mark.parametrize("name", ["cfg1_1k", "g10k"])
+def test_cli_icp_vs_reference(icp, golden_icp, golden_meta, name):
+    m = golden_meta["icp_cli"][name]
+    R, t, tcums, out = icp.cli_icp(golden_icp[f"{name}_source"], golden_icp[f"{name}_target"],
+                                   m["iterations"], m["tolerance"], device=0)
+    ref = golden_icp[f"{name}_T_cums"]
+    assert tcums.shape == ref.shape
+    assert t_rmse(tcums[-1], ref[-1]) < RMSE_TOL
+    np.testing.assert_allclose(tcums, ref, atol=1e-9)
+    np.testing.assert_allclose(R, golden_icp[f"{name}_R_final"], atol=1e-9)  # last incremental T quirk
+    np.testing.assert_allclose(t, golden_icp[f"{name}_t_final"], atol=1e-9)
+    np.testing.assert_allclose(out, golden_icp[f"{name}_source_out"], atol=1e-8)
+
+
+@pytest.mark.parametrize("n,yaw", [(5000, 2.0), (30000, 6.0)])
+def test_engine_register_vs_oracle(icp, oracle, n, yaw):
+    tgt, src, T_true = icp.synth_pair(n, yaw_deg=yaw)
+    p = icp.params_default(max_iterations=50, tolerance=1e-9)
+    rc, res, hist, out = icp.engine_register(p, src, tgt, device=0)
+    orc, ores, ohist, oout = oracle.icp(src, tgt, oracle.SEM_ENGINE, 50, 1e-9)
+    assert rc == 0 and orc == 0 and res.success
+    assert res.total_iterations == ores.total_iterations
+    assert [h.valid_points for h in hist] == [h.valid for h in ohist]
+    T = np.eye(4)
+    T[:3, :3] = np.array(res.final_R).reshape(3, 3)
+    T[:3, 3] = res.final_t
+    To = np.eye(4)
+    To[:3, :3] = np.array(ores.final_R).reshape(3, 3)
+    To[:3, 3] = ores.final_t
+    assert t_rmse(T, To) < RMSE_TOL
+    np.testing.assert_allclose(T, To, atol=1e-10)
+    np.testing.assert_allclose(res.final_rmse, ores.final_rmse, rtol=1e-9, atol=1e-15)
+    np.testing.assert_allclose(out, oout, atol=1e-9)
+    for h, o in zip(hist, ohist):
+        np.testing.assert_allclose(np.array(h.transform), np.array(o.T_cum), atol=1e-10)
+
+
+def test_engine_too_few_pairs_keeps_source(icp):
+    tgt = np.random.default_rng(1).normal(size=(100, 3))
+    src = tgt[:2] + 0.01  # 2 points: valid < 3 on the first iteration
+    p = icp.params_default()
+    rc, res, hist, out = icp.engine_register(p, src, tgt, device=0)
+    assert rc == -11 and not res.success  # ICP_ENGINE_TOO_FEW, finished(false) (icpengine.cpp:319-323)
+    np.testing.assert_array_equal(out, src)  # no write-back
+    R, t, tr, out2 = icp.cli_icp(src, tgt, 20, 1e-2, device=0)  # CLI breaks and writes back
+    np.testing.assert_array_equal(R, np.eye(3))
+    np.testing.assert_array_equal(out2, src)
+
+
+def test_engine_stop_flag(icp):
+    import ctypes
+    tgt, src, _ = icp.synth_pair(5000)
+    flag = ctypes.c_int32(1)
+    rc, res, hist, out = icp.engine_register(icp.params_default(), src, tgt, device=0, stop_flag=flag)
+    assert rc == -10 and res.status == 4 and not res.success
+    np.testing.assert_array_equal(out, src)
+
+
+def test_empty_inputs_rejected(icp):
+    p = icp.params_default()
+    rc, res, _, _ = icp.engine_register(p, np.zeros((0, 3)), np.ones((5, 3)), device=0)
+    assert rc != 0 and not res.success  # icpengine.cpp:31-34
+    rc, res, _, _ = icp.engine_register(p, np.ones((5, 3)), np.zeros((0, 3)), device=0)
+    assert rc != 0 and not res.success
