@@ -59,13 +59,24 @@ def test_fullsize_iteration_deterministic(icp, gpu_ctx, big):
     assert a.as_dict() == b.as_dict()
 
 
-def test_fullsize_registration_recovers_motion(icp, gpu_ctx, big):
-    _, _, T_true = big
+def test_fullsize_registration_runs(icp, gpu_ctx, big):
+    """30 engine iterations at 10M: RMSE falls and the loop finishes. (The config-4 cloud is a
+    N(0, diag(5,5,1)^2) blob: symmetric under yaw, so the 5 deg yaw is not observable by any
+    ICP; recovery of a known motion is tested on an anisotropic cloud below.)"""
     p = icp.params_default(max_iterations=30, tolerance=1e-10)
     rc, res, hist = gpu_ctx.run(p)
     assert rc == 0 and res.success
-    R = np.array(res.final_R).reshape(3, 3)
-    # 1 % outliers + 1 mm noise: the estimate sits within a few micro-radians of the truth
-    np.testing.assert_allclose(R, T_true[:3, :3], atol=1e-4)
-    np.testing.assert_allclose(np.array(res.final_t), T_true[:3, 3], atol=1e-3)
     assert hist[-1].rmse < hist[0].rmse
+    assert all(h.valid_points > 0.95 * N for h in hist)
+
+
+def test_registration_recovers_known_motion(icp):
+    tgt, src, T_true = icp.synth_pair(1_000_000, sigma=[8.0, 4.0, 1.5], yaw_deg=1.0, pitch_deg=0.5,
+                                      roll_deg=-0.3, t=[0.05, -0.03, 0.02], noise_sigma=0.0,
+                                      outlier_fraction=0.0)
+    p = icp.params_default(max_iterations=100, tolerance=1e-12)
+    rc, res, hist, out = icp.engine_register(p, src, tgt, device=0)
+    assert rc == 0 and res.success
+    np.testing.assert_allclose(np.array(res.final_R).reshape(3, 3), T_true[:3, :3], atol=1e-6)
+    np.testing.assert_allclose(np.array(res.final_t), T_true[:3, 3], atol=1e-6)
+    assert res.final_rmse < 1e-6

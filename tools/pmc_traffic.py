@@ -1,0 +1,69 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 output of the bench into profiles/ (HBM traffic per search launch).
+
+Reads the kernel-trace stats and the counter-collection CSVs written by tools/profile_bench.sh
+and applies the gfx950 correction of MI355X_MICROARCH.md §HBM: FETCH_SIZE/WRITE_SIZE are KiB;
+FETCH_SIZE reports 1/2 of the bytes of wide (16 B/lane) reads, so reads are doubled.
+
+usage: pmc_traffic.py PROF_DIR N WORLD  -> JSON on stdout
+"""
+import csv
+import glob
+import json
+import sys
+from collections import defaultdict
+
+KERNEL = "k_nn<true, false>"
+
+
+def rows(pattern):
+    out = []
+    for f in glob.glob(pattern, recursive=True):
+        with open(f, newline="") as fh:
+            out.extend(csv.DictReader(fh))
+    return out
+
+
+def per_dispatch(prof, sub):
+    vals = defaultdict(lambda: defaultdict(float))
+    for r in rows(f"{prof}/{sub}/**/*counter_collection.csv"):
+        if KERNEL not in r.get("Kernel_Name", ""):
+            continue
+        vals[r["Counter_Name"]][r["Dispatch_Id"]] += float(r["Counter_Value"])
+    return {k: (sum(v.values()) / len(v), len(v)) for k, v in vals.items() if v}
+
+
+def main():
+    prof, n, world = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
+    import hashlib
+    from pathlib import Path
+    src = Path(__file__).resolve().parents[1] / "iterativeclosestpoint_amd" / "csrc" / "kernels.hip"
+    out = {"kernel": KERNEL, "n": n, "world": world,
+           "kernels_hip_sha1": hashlib.sha1(src.read_bytes()).hexdigest()}
+    stats = rows(f"{prof}/trace/**/*kernel_stats.csv")
+    for r in stats:
+        if KERNEL in r.get("Name", r.get("KernelName", "")):
+            out["trace_calls"] = int(r["Calls"])
+            out["trace_avg_ms"] = float(r["AverageNs"]) / 1e6
+            out["trace_min_ms"] = float(r["MinNs"]) / 1e6
+            out["trace_max_ms"] = float(r["MaxNs"]) / 1e6
+    fetch = per_dispatch(prof, "pmc_fetch").get("FETCH_SIZE")
+    write = per_dispatch(prof, "pmc_write").get("WRITE_SIZE")
+    hits = per_dispatch(prof, "pmc_l2")
+    if fetch:
+        out["fetch_size_kib_raw"] = fetch[0]
+        out["fetch_bytes_corrected"] = fetch[0] * 1024 * 2
+        out["pmc_dispatches"] = fetch[1]
+    if write:
+        out["write_size_kib_raw"] = write[0]
+        out["write_bytes"] = write[0] * 1024
+    if fetch and write:
+        out["hbm_bytes_per_launch"] = out["fetch_bytes_corrected"] + out["write_bytes"]
+    if "TCC_HIT_sum" in hits and "TCC_MISS_sum" in hits:
+        h, m = hits["TCC_HIT_sum"][0], hits["TCC_MISS_sum"][0]
+        out["l2_hit_rate"] = h / (h + m) if h + m else None
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()

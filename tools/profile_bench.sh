@@ -1,0 +1,23 @@
+#!/bin/bash
+# Profile the bench command with rocprofv3 (kernel trace + stats; then separate PMC passes).
+# usage (on the GPU box, from the repo root): bash tools/profile_bench.sh TAG [N]
+set -u
+TAG=${1:-r01}
+N=${2:-10000000}
+REPO=$(pwd)
+OUT=$REPO/gpurun_out/prof_$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+BENCH="$REPO/bench.py --n $N --no-cpu-baseline"
+cd /tmp
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o "$TAG" -- \
+  python3 $BENCH --steps 10 --warmup 3 > "$OUT/bench_traced.json" 2> "$OUT/trace.err" || exit $?
+timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o "$TAG" -- \
+  python3 $BENCH --steps 3 --warmup 1 > /dev/null 2> "$OUT/pmc_fetch.err" || exit $?
+timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o "$TAG" -- \
+  python3 $BENCH --steps 3 --warmup 1 > /dev/null 2> "$OUT/pmc_write.err" || exit $?
+timeout -k 10 600 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv -d "$OUT/pmc_l2" -o "$TAG" -- \
+  python3 $BENCH --steps 3 --warmup 1 > /dev/null 2> "$OUT/pmc_l2.err" || exit $?
+cd "$REPO"
+python3 tools/pmc_traffic.py "$OUT" "$N" 1 > "$OUT/traffic.json"
+cat "$OUT/traffic.json"
