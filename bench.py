@@ -116,13 +116,14 @@ def main() -> int:
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("gloo", rank=rank, world_size=world)
-    torch.cuda.set_device(local_rank)
+    device = local_rank % max(1, torch.cuda.device_count())  # ranks > GPUs only in rehearsals
+    torch.cuda.set_device(device)
 
     n = args.n
     t_setup = time.perf_counter()
     tgt, src, T_true = icp.synth_pair(n)
     lo, hi = shard_range(n, rank, world)
-    ctx = icp.Context(local_rank)
+    ctx = icp.Context(device)
     ctx.set_target(tgt, 10, 20, icp.RULES_ENGINE)
     ctx.set_source(src[lo:hi])
     if world > 1:
@@ -144,7 +145,7 @@ def main() -> int:
     it_ms = []
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        sess.step()
+        rec = sess.step()
         a, b = ctx.last_timing()
         nn_ms.append(a)
         it_ms.append(b)
@@ -161,6 +162,7 @@ def main() -> int:
 
     # untimed: reference-DFS work of this rank's queries (the V, P of the byte model)
     v_mean, p_mean = ctx.traversal_counts()
+    probe = ctx.iterate(None, 1, icp.RULES_ENGINE, 3.0)  # untimed: fallback share of the final state
     n_local = hi - lo
     nn_avg_s = float(np.mean(nn_ms)) / 1e3
     b_corr = bytes_per_corr(v_mean, p_mean)
@@ -217,6 +219,7 @@ def main() -> int:
                 "bytes_per_corr": round(b_corr, 1), "node_entries_per_query": round(v_mean, 3),
                 "leaf_points_per_query": round(p_mean, 3), "kernel_ms_avg": round(float(np.mean(nn_ms)), 4),
                 "iterate_device_ms_avg": round(float(np.mean(it_ms)), 4),
+                "exact_fallback_queries": int(probe.n_fallback),
             },
             "cpu_baseline": cpu,
             "setup_s": round(setup_s, 2),

@@ -61,6 +61,8 @@ typedef struct icp_iter_stats {
   double centroid_src[3]; /* mean of valid source points     icpengine.cpp:82     */
   double centroid_tgt[3]; /* mean of matched target points   icpengine.cpp:83     */
   double H[9];        /* sum (a-ca)(b-cb)^T row-major        icpengine.cpp:86-90  */
+  int64_t n_fallback; /* this rank's queries the certified fast search handed to the exact
+                         reference-order DFS (near-ties)                     */
 } icp_iter_stats;
 
 int icp_hip_device_count(int* count);

@@ -12,6 +12,7 @@
 
 #include <cfloat>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -69,6 +70,7 @@ static void free_source(icp_hip_ctx* c) {
   dfree(c->perm);
   dfree(c->pos);
   dfree(c->dist);
+  dfree(c->fb_list);
   dfree(c->mparts);
   dfree(c->cparts);
   c->n_src = 0;
@@ -99,13 +101,15 @@ int icp_hip_create(icp_hip_ctx** out, int device) {
   HIP_TRY(hipSetDevice(device));
   icp_hip_ctx* c = new icp_hip_ctx();
   c->device = device;
+  if (const char* v = std::getenv("ICP_NN_VARIANT")) c->nn_variant = std::atoi(v);
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
     delete c;
     return fail(ICP_HIP_EDEVICE, "hipStreamCreate failed");
   }
   for (hipEvent_t* ev : {&c->ev_it0, &c->ev_it1, &c->ev_nn0, &c->ev_nn1}) (void)hipEventCreate(ev);
   if (dalloc(&c->it, 1) != hipSuccess || hipHostMalloc(reinterpret_cast<void**>(&c->h_it), sizeof(IterDev)) != hipSuccess ||
-      dalloc(&c->counters, 2) != hipSuccess || dalloc(&c->Tbuf, 16) != hipSuccess) {
+      dalloc(&c->counters, 2) != hipSuccess || dalloc(&c->Tbuf, 16) != hipSuccess ||
+      dalloc(&c->fb_count, 2) != hipSuccess) {
     icp_hip_destroy(c);
     return fail(ICP_HIP_ENOMEM, "context allocation failed");
   }
@@ -123,6 +127,7 @@ void icp_hip_destroy(icp_hip_ctx* c) {
   dfree(c->it);
   dfree(c->counters);
   dfree(c->Tbuf);
+  dfree(c->fb_count);
   dfree(c->gm);
   dfree(c->gc);
   if (c->h_it) (void)hipHostFree(c->h_it);
@@ -200,6 +205,7 @@ int icp_hip_set_source(icp_hip_ctx* c, const double* xyz, int64_t n) {
   HIP_TRY(dalloc(&c->perm, n));
   HIP_TRY(dalloc(&c->pos, n));
   HIP_TRY(dalloc(&c->dist, n));
+  HIP_TRY(dalloc(&c->fb_list, n));
   HIP_TRY(dalloc(&c->mparts, (size_t)(c->nb_nn + 2 * ((c->nb_nn + 255) / 256) + 4)));
   HIP_TRY(dalloc(&c->cparts, (size_t)(c->nb_cull + 2 * ((c->nb_cull + 255) / 256) + 4)));
   if (n == 0) return ICP_HIP_OK;
@@ -275,12 +281,17 @@ int icp_hip_iterate(icp_hip_ctx* c, const double* T_apply, int iter, int rules, 
   a.pos0 = c->pos0;
   a.levels = c->levels;
   a.init_best = c->init_best;
+  a.variant = c->nn_variant;
   a.apply = T_apply ? 1 : 0;
   if (T_apply)
     for (int k = 0; k < 12; k++) a.T[k] = T_apply[k];
+  a.fb_list = c->fb_list;
+  a.fb_count = c->fb_count;
+  HIP_TRY(hipMemsetAsync(c->fb_count, 0, sizeof(unsigned int), s));
   HIP_TRY(hipEventRecord(c->ev_nn0, s));
+  a.ev_fast_done = c->nn_variant == 3 ? c->ev_nn1 : nullptr;
   HIP_TRY(launch_nn(a, s));
-  HIP_TRY(hipEventRecord(c->ev_nn1, s));
+  if (c->nn_variant != 3) HIP_TRY(hipEventRecord(c->ev_nn1, s));
   HIP_TRY(launch_merge_moments(c->mparts, c->nb_nn, &c->it->m_local, s));
   const bool multi = c->nranks > 1;
   if (multi)
@@ -303,6 +314,7 @@ int icp_hip_iterate(icp_hip_ctx* c, const double* T_apply, int iter, int rules, 
     RCCL_TRY(ncclAllGather(&c->it->c_local, c->gc, sizeof(CovMoments) / sizeof(double), ncclDouble, c->comm, s));
   HIP_TRY(launch_finalize_cov(multi ? c->gc : nullptr, multi ? c->nranks : 1, c->it, s));
   HIP_TRY(hipMemcpyAsync(c->h_it, c->it, sizeof(IterDev), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(&c->last_fallbacks, c->fb_count, sizeof(unsigned int), hipMemcpyDeviceToHost, s));
   HIP_TRY(hipEventRecord(c->ev_it1, s));
   HIP_TRY(hipStreamSynchronize(s));
   const IterDev& h = *c->h_it;
@@ -321,6 +333,7 @@ int icp_hip_iterate(icp_hip_ctx* c, const double* T_apply, int iter, int rules, 
     out->centroid_tgt[k] = h.c_global.mb[k];
   }
   for (int k = 0; k < 9; k++) out->H[k] = h.c_global.c[k];
+  out->n_fallback = c->nn_variant == 3 ? (int64_t)c->last_fallbacks : 0;
   c->have_results = true;
   return ICP_HIP_OK;
 }
@@ -396,7 +409,17 @@ int icp_hip_nn(icp_hip_ctx* c, const double* q, int64_t n, int32_t* idx_out, dou
     a.pos0 = c->pos0;
     a.levels = c->levels;
     a.init_best = c->init_best;
+  a.variant = c->nn_variant;
+    int32_t* fbl = nullptr;
+    if (e == hipSuccess) e = dalloc(&fbl, n);
+    a.fb_list = fbl;
+    a.fb_count = c->fb_count;
+    if (e == hipSuccess) e = hipMemsetAsync(c->fb_count, 0, sizeof(unsigned int), c->stream);
     if (e == hipSuccess) e = launch_nn(a, c->stream);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(&c->last_fallbacks, c->fb_count, sizeof(unsigned int), hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    dfree(fbl);
     if (e == hipSuccess) e = launch_scatter_corr(nullptr, pos, c->pts, di, d, dd, n, c->stream);
     if (e == hipSuccess && idx_out) e = hipMemcpyAsync(idx_out, di, sizeof(int32_t) * n, hipMemcpyDeviceToHost, c->stream);
     if (e == hipSuccess && dist_out) e = hipMemcpyAsync(dist_out, dd, sizeof(double) * n, hipMemcpyDeviceToHost, c->stream);
@@ -428,6 +451,7 @@ int icp_hip_traversal_counts(icp_hip_ctx* c, double* mean_entries, double* mean_
   a.pos0 = c->pos0;
   a.levels = c->levels;
   a.init_best = c->init_best;
+  a.variant = c->nn_variant;
   a.count = 1;
   HIP_TRY(launch_nn(a, c->stream));
   unsigned long long h[2] = {0, 0};

@@ -10,6 +10,7 @@
 
 struct icp_hip_ctx {
   int device = 0;
+  int nn_variant = 3;  // search kernel variant (ICP_NN_VARIANT env, for A/B runs)
   hipStream_t stream = nullptr;
   hipEvent_t ev_it0 = nullptr, ev_it1 = nullptr, ev_nn0 = nullptr, ev_nn1 = nullptr;
 
@@ -26,6 +27,9 @@ struct icp_hip_ctx {
   int32_t* perm = nullptr;
   int32_t* pos = nullptr;  // leaf-order position of the match
   double* dist = nullptr;  // residual
+  int32_t* fb_list = nullptr;            // queries for the exact fallback
+  unsigned int* fb_count = nullptr;
+  unsigned int last_fallbacks = 0;
   icp::Moments* mparts = nullptr;
   icp::CovMoments* cparts = nullptr;
   int64_t nb_nn = 0, nb_cull = 0;

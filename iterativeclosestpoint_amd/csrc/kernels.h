@@ -39,6 +39,10 @@ struct NNLaunch {
   double T[12];                    // row-major 3x4, used when apply != 0
   int apply;
   int count;
+  int variant;  // 1 = k_nn (reference order), 2 = k_nn2, 3 = certified fast path + fallback
+  int32_t* fb_list;        // variant 3: queries sent to the exact fallback
+  unsigned int* fb_count;  // zeroed before the launch
+  hipEvent_t ev_fast_done; // optional: recorded right after the fast kernel
 };
 
 // Threads per block of the NN kernel for a given stack depth.

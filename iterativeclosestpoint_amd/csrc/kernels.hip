@@ -83,136 +83,32 @@ __device__ __forceinline__ uint64_t pack_entry(int32_t first, uint32_t ranks, ui
   return ((uint64_t)(ranks | (cnt << 24)) << 32) | (uint32_t)first;
 }
 
-template <bool APPLY, bool COUNT>
-__global__ void __launch_bounds__(256) k_nn(NNLaunch a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned long long lds_stack[];
-  const int bs = blockDim.x;
-  const int64_t i = (int64_t)blockIdx.x * bs + threadIdx.x;
-  const bool active = i < a.n;
-
-  double qx = 0.0, qy = 0.0, qz = 0.0;
-  if (active) {
-    qx = a.x[i];
-    qy = a.y[i];
-    qz = a.z[i];
-    if (APPLY) {
-      // src = T * src, Eigen order ((T0 x + T1 y) + T2 z) + T3 (icpengine.cpp:345)
-      const double nx = ((a.T[0] * qx + a.T[1] * qy) + a.T[2] * qz) + a.T[3];
-      const double ny = ((a.T[4] * qx + a.T[5] * qy) + a.T[6] * qz) + a.T[7];
-      const double nz = ((a.T[8] * qx + a.T[9] * qy) + a.T[10] * qz) + a.T[11];
-      a.x[i] = nx;
-      a.y[i] = ny;
-      a.z[i] = nz;
-      qx = nx;
-      qy = ny;
-      qz = nz;
-    }
+template <bool APPLY>
+__device__ __forceinline__ void nn_load_query(const NNLaunch& a, int64_t i, bool active, double& qx, double& qy,
+                                              double& qz) {
+  if (!active) return;
+  qx = a.x[i];
+  qy = a.y[i];
+  qz = a.z[i];
+  if (APPLY) {
+    // src = T * src, Eigen order ((T0 x + T1 y) + T2 z) + T3 (icpengine.cpp:345)
+    const double nx = ((a.T[0] * qx + a.T[1] * qy) + a.T[2] * qz) + a.T[3];
+    const double ny = ((a.T[4] * qx + a.T[5] * qy) + a.T[6] * qz) + a.T[7];
+    const double nz = ((a.T[8] * qx + a.T[9] * qy) + a.T[10] * qz) + a.T[11];
+    a.x[i] = nx;
+    a.y[i] = ny;
+    a.z[i] = nz;
+    qx = nx;
+    qy = ny;
+    qz = nz;
   }
+}
 
-  double best_d2 = a.init_best;
-  int32_t best = -1;
-  double visits = 0.0, scanned = 0.0;
-  // A NaN coordinate makes every leaf distance NaN, so the reference never updates best_idx
-  // (octree.cpp:146): skipping the search is exact. (Its box distances stay finite: max(0,NaN)=0.)
-  const bool nan_q = (qx != qx) || (qy != qy) || (qz != qz);
-  if (active && !nan_q && a.n_nodes > 0) {
-    unsigned long long* st = lds_stack + threadIdx.x;
-    int sp = 0;
-    int32_t node = 0;
-    bool siblings_on_top = false;
-    if (COUNT) visits += 1.0;
-    while (true) {
-      const NodeRec* r = a.nodes + node;
-      const double2 l01 = *reinterpret_cast<const double2*>(&r->lo[0]);
-      const double2 l2h0 = *reinterpret_cast<const double2*>(&r->lo[2]);
-      const double2 h12 = *reinterpret_cast<const double2*>(&r->hi[1]);
-      const int4 topo = *reinterpret_cast<const int4*>(&r->first);
-      const double lx = l01.x, ly = l01.y, lz = l2h0.x, hx = l2h0.y, hy = h12.x, hz = h12.y;
-      const double m = box_dist(lx, ly, lz, hx, hy, hz, qx, qy, qz);
-      const int32_t first = topo.x;
-      const uint32_t meta = (uint32_t)topo.y;
-      if (m * m >= best_d2) {
-        // Pruned (octree.cpp:134-135). Siblings still pending on the top level come later in
-        // ascending distance, so they would all be pruned too: drop the level (exact).
-        if (siblings_on_top) sp--;
-      } else if (meta & kLeafBit) {
-        const int32_t cnt = (int32_t)(meta & ~kLeafBit);
-        if (COUNT) scanned += (double)cnt;
-        for (int32_t k = 0; k < cnt; k++) {
-          const TgtPt* p = a.pts + first + k;
-          const double2 pxy = *reinterpret_cast<const double2*>(&p->x);
-          const double pz = p->z;
-          const double dx = pxy.x - qx;
-          const double dy = pxy.y - qy;
-          const double dz = pz - qz;
-          const double d2 = dx * dx + dy * dy + dz * dz;
-          if (d2 < best_d2) {  // strict <, ascending original index inside a leaf
-            best_d2 = d2;
-            best = first + k;
-          }
-        }
-      } else {
-        // Inner node: distances of the existing children from the parent box and its
-        // midpoint (the stored child boxes are exactly these values, octree.cpp:97-120).
-        const double mx = (lx + hx) / 2, my = (ly + hy) / 2, mz = (lz + hz) / 2;
-        const double ax0 = smax(0.0, smax(lx - qx, qx - mx)), ax1 = smax(0.0, smax(mx - qx, qx - hx));
-        const double ay0 = smax(0.0, smax(ly - qy, qy - my)), ay1 = smax(0.0, smax(my - qy, qy - hy));
-        const double az0 = smax(0.0, smax(lz - qz, qz - mz)), az1 = smax(0.0, smax(mz - qz, qz - hz));
-        const double sx[2] = {ax0 * ax0, ax1 * ax1};
-        const double sy[2] = {ay0 * ay0, ay1 * ay1};
-        const double sz[2] = {az0 * az0, az1 * az1};
-        const uint32_t mask = meta & 0xffu;
-        double cd[8];
-#pragma unroll
-        for (int o = 0; o < 8; o++) cd[o] = __builtin_sqrt(sx[o & 1] + sy[(o >> 1) & 1] + sz[o >> 2]);
-        // Stable order = sort by (distance, octant): rank = #children strictly before.
-        uint32_t rk[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-#pragma unroll
-        for (int p = 0; p < 8; p++) {
-#pragma unroll
-          for (int q = p + 1; q < 8; q++) {
-            const bool both = ((mask >> p) & 1u) && ((mask >> q) & 1u);
-            const bool q_first = cd[q] < cd[p];
-            rk[p] += (both && q_first) ? 1u : 0u;
-            rk[q] += (both && !q_first) ? 1u : 0u;
-          }
-        }
-        uint32_t ranks = 0;
-#pragma unroll
-        for (int o = 0; o < 8; o++) {
-          if ((mask >> o) & 1u) {
-            const uint32_t block_slot = (uint32_t)__builtin_popcount(mask & ((1u << o) - 1u));
-            ranks |= block_slot << (3u * rk[o]);
-          }
-        }
-        const uint32_t nch = (uint32_t)__builtin_popcount(mask);
-        if (COUNT) visits += (double)nch;
-        node = first + (int32_t)(ranks & 7u);
-        if (nch > 1) {
-          st[sp * bs] = pack_entry(first, ranks >> 3, nch - 1);
-          sp++;
-          siblings_on_top = true;
-        } else {
-          siblings_on_top = false;
-        }
-        continue;
-      }
-      if (sp == 0) break;
-      const unsigned long long e = st[(sp - 1) * bs];
-      const int32_t base = (int32_t)(uint32_t)e;
-      const uint32_t hi = (uint32_t)(e >> 32);
-      const uint32_t rem = (hi >> 24) - 1u;
-      node = base + (int32_t)(hi & 7u);
-      if (rem == 0) {
-        sp--;
-        siblings_on_top = false;
-      } else {
-        st[(sp - 1) * bs] = pack_entry(base, (hi & 0xffffffu) >> 3, rem);
-        siblings_on_top = true;
-      }
-    }
-  }
-
+// Residual, outputs, per-block residual moments (and work counters in COUNT mode).
+template <bool COUNT>
+__device__ __forceinline__ void nn_finish(const NNLaunch& a, int64_t i, bool active, double qx, double qy,
+                                          double qz, int32_t best, double best_d2, double visits, double scanned,
+                                          unsigned long long* lds_stack) {
   int32_t pos = best;
   double d = 0.0;
   if (active) {
@@ -262,6 +158,571 @@ __global__ void __launch_bounds__(256) k_nn(NNLaunch a) {
       atomicAdd(&a.counters[0], (unsigned long long)c[0]);
       atomicAdd(&a.counters[1], (unsigned long long)c[1]);
     }
+  }
+}
+
+// The reference DFS (Octree::searchNearest, octree.cpp:128-173) for one query, verbatim order:
+// box distance with its sqrt, prune m*m >= best, children in stable ascending-distance order,
+// strict < in leaf scans. `st` is this thread's column of the LDS level stack (stride bs).
+template <bool COUNT>
+__device__ __forceinline__ void exact_dfs(const NNLaunch& a, double qx, double qy, double qz, unsigned long long* st,
+                                          int bs, int32_t& best, double& best_d2, double& visits,
+                                          double& scanned) {
+  int sp = 0;
+  int32_t node = 0;
+  bool siblings_on_top = false;
+  if (COUNT) visits += 1.0;
+  while (true) {
+    const NodeRec* r = a.nodes + node;
+    const double2 l01 = *reinterpret_cast<const double2*>(&r->lo[0]);
+    const double2 l2h0 = *reinterpret_cast<const double2*>(&r->lo[2]);
+    const double2 h12 = *reinterpret_cast<const double2*>(&r->hi[1]);
+    const int4 topo = *reinterpret_cast<const int4*>(&r->first);
+    const double lx = l01.x, ly = l01.y, lz = l2h0.x, hx = l2h0.y, hy = h12.x, hz = h12.y;
+    const double m = box_dist(lx, ly, lz, hx, hy, hz, qx, qy, qz);
+    const int32_t first = topo.x;
+    const uint32_t meta = (uint32_t)topo.y;
+    if (m * m >= best_d2) {
+      // Pruned (octree.cpp:134-135). Siblings still pending on the top level come later in
+      // ascending distance, so they would all be pruned too: drop the level (exact).
+      if (siblings_on_top) sp--;
+    } else if (meta & kLeafBit) {
+      const int32_t cnt = (int32_t)(meta & ~kLeafBit);
+      if (COUNT) scanned += (double)cnt;
+      for (int32_t k = 0; k < cnt; k++) {
+        const TgtPt* p = a.pts + first + k;
+        const double2 pxy = *reinterpret_cast<const double2*>(&p->x);
+        const double pz = p->z;
+        const double dx = pxy.x - qx;
+        const double dy = pxy.y - qy;
+        const double dz = pz - qz;
+        const double d2 = dx * dx + dy * dy + dz * dz;
+        if (d2 < best_d2) {  // strict <, ascending original index inside a leaf
+          best_d2 = d2;
+          best = first + k;
+        }
+      }
+    } else {
+      // Inner node: distances of the existing children from the parent box and its
+      // midpoint (the stored child boxes are exactly these values, octree.cpp:97-120).
+      const double mx = (lx + hx) / 2, my = (ly + hy) / 2, mz = (lz + hz) / 2;
+      const double ax0 = smax(0.0, smax(lx - qx, qx - mx)), ax1 = smax(0.0, smax(mx - qx, qx - hx));
+      const double ay0 = smax(0.0, smax(ly - qy, qy - my)), ay1 = smax(0.0, smax(my - qy, qy - hy));
+      const double az0 = smax(0.0, smax(lz - qz, qz - mz)), az1 = smax(0.0, smax(mz - qz, qz - hz));
+      const double sx[2] = {ax0 * ax0, ax1 * ax1};
+      const double sy[2] = {ay0 * ay0, ay1 * ay1};
+      const double sz[2] = {az0 * az0, az1 * az1};
+      const uint32_t mask = meta & 0xffu;
+      double cd[8];
+#pragma unroll
+      for (int o = 0; o < 8; o++) cd[o] = __builtin_sqrt(sx[o & 1] + sy[(o >> 1) & 1] + sz[o >> 2]);
+      // Stable order = sort by (distance, octant): rank = #children strictly before.
+      uint32_t rk[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+      for (int p = 0; p < 8; p++) {
+#pragma unroll
+        for (int q = p + 1; q < 8; q++) {
+          const bool both = ((mask >> p) & 1u) && ((mask >> q) & 1u);
+          const bool q_first = cd[q] < cd[p];
+          rk[p] += (both && q_first) ? 1u : 0u;
+          rk[q] += (both && !q_first) ? 1u : 0u;
+        }
+      }
+      uint32_t ranks = 0;
+#pragma unroll
+      for (int o = 0; o < 8; o++) {
+        if ((mask >> o) & 1u) {
+          const uint32_t block_slot = (uint32_t)__builtin_popcount(mask & ((1u << o) - 1u));
+          ranks |= block_slot << (3u * rk[o]);
+        }
+      }
+      const uint32_t nch = (uint32_t)__builtin_popcount(mask);
+      if (COUNT) visits += (double)nch;
+      node = first + (int32_t)(ranks & 7u);
+      if (nch > 1) {
+        st[sp * bs] = pack_entry(first, ranks >> 3, nch - 1);
+        sp++;
+        siblings_on_top = true;
+      } else {
+        siblings_on_top = false;
+      }
+      continue;
+    }
+    if (sp == 0) break;
+    const unsigned long long e = st[(sp - 1) * bs];
+    const int32_t base = (int32_t)(uint32_t)e;
+    const uint32_t hi = (uint32_t)(e >> 32);
+    const uint32_t rem = (hi >> 24) - 1u;
+    node = base + (int32_t)(hi & 7u);
+    if (rem == 0) {
+      sp--;
+      siblings_on_top = false;
+    } else {
+      st[(sp - 1) * bs] = pack_entry(base, (hi & 0xffffffu) >> 3, rem);
+      siblings_on_top = true;
+    }
+  }
+}
+
+template <bool APPLY, bool COUNT>
+__global__ void __launch_bounds__(256) k_nn(NNLaunch a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned long long lds_stack[];
+  const int bs = blockDim.x;
+  const int64_t i = (int64_t)blockIdx.x * bs + threadIdx.x;
+  const bool active = i < a.n;
+
+  double qx = 0.0, qy = 0.0, qz = 0.0;
+  nn_load_query<APPLY>(a, i, active, qx, qy, qz);
+
+  double best_d2 = a.init_best;
+  int32_t best = -1;
+  double visits = 0.0, scanned = 0.0;
+  // A NaN coordinate makes every leaf distance NaN, so the reference never updates best_idx
+  // (octree.cpp:146): skipping the search is exact. (Its box distances stay finite: max(0,NaN)=0.)
+  const bool nan_q = (qx != qx) || (qy != qy) || (qz != qz);
+  if (active && !nan_q && a.n_nodes > 0)
+    exact_dfs<COUNT>(a, qx, qy, qz, lds_stack + threadIdx.x, bs, best, best_d2, visits, scanned);
+  nn_finish<COUNT>(a, i, active, qx, qy, qz, best, best_d2, visits, scanned, lds_stack);
+}
+
+// Exact form of the prune test m*m >= best with m = sqrt(s) (octree.cpp:134-135), without the
+// sqrt in the common case: fl(fl(sqrt(s))^2) lies within a relative 3*2^-53 of s, so outside a
+// 2^-48 band around best (normal range) the answer is decided by s alone; inside it, the
+// reference arithmetic is evaluated literally.
+__device__ __forceinline__ bool prune_test(double s, double best) {
+  constexpr double kTiny = 0x1p-900;
+  if (s >= kTiny) {
+    if (s > best * (1.0 + 0x1p-48)) return true;
+    if (best >= kTiny && s < best * (1.0 - 0x1p-48)) return false;
+  }
+  const double m = __builtin_sqrt(s);
+  return m * m >= best;
+}
+
+// v2: same DFS as k_nn with
+//  * prune_test() instead of a sqrt per node entry;
+//  * children ranked by their squared box distance s (ties -> lower octant); sqrt is monotone,
+//    so this equals the reference's stable sort on sqrt(s) unless two distinct s collide under
+//    sqrt, which needs them within 2^-51 relative: such near-ties switch to ranking by sqrt(s);
+//  * the nearest child is entered straight from registers: its box is the parent box split at
+//    the midpoint (the stored child boxes are exactly these values), so only its 8-byte
+//    topology word is loaded. Popped siblings load their 48-byte box.
+template <bool APPLY, bool COUNT>
+__global__ void __launch_bounds__(256) k_nn2(NNLaunch a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned long long lds_stack[];
+  const int bs = blockDim.x;
+  const int64_t i = (int64_t)blockIdx.x * bs + threadIdx.x;
+  const bool active = i < a.n;
+
+  double qx = 0.0, qy = 0.0, qz = 0.0;
+  nn_load_query<APPLY>(a, i, active, qx, qy, qz);
+
+  double best_d2 = a.init_best;
+  int32_t best = -1;
+  double visits = 0.0, scanned = 0.0;
+  const bool nan_q = (qx != qx) || (qy != qy) || (qz != qz);  // see k_nn
+  if (active && !nan_q && a.n_nodes > 0) {
+    unsigned long long* st = lds_stack + threadIdx.x;
+    int sp = 0;
+    int32_t node = 0;
+    bool siblings_on_top = false;
+    bool have_box = false;  // box registers + s valid for `node`
+    double lx = 0, ly = 0, lz = 0, hx = 0, hy = 0, hz = 0, s_node = 0;
+    if (COUNT) visits += 1.0;
+    while (true) {
+      const NodeRec* r = a.nodes + node;
+      if (!have_box) {
+        const double2 l01 = *reinterpret_cast<const double2*>(&r->lo[0]);
+        const double2 l2h0 = *reinterpret_cast<const double2*>(&r->lo[2]);
+        const double2 h12 = *reinterpret_cast<const double2*>(&r->hi[1]);
+        lx = l01.x; ly = l01.y; lz = l2h0.x; hx = l2h0.y; hy = h12.x; hz = h12.y;
+        const double dx = smax(0.0, smax(lx - qx, qx - hx));
+        const double dy = smax(0.0, smax(ly - qy, qy - hy));
+        const double dz = smax(0.0, smax(lz - qz, qz - hz));
+        s_node = dx * dx + dy * dy + dz * dz;
+      }
+      bool descend = false;
+      if (prune_test(s_node, best_d2)) {
+        // every pending sibling is at least as far: the reference would prune them all
+        if (siblings_on_top) sp--;
+      } else {
+        const int2 topo = *reinterpret_cast<const int2*>(&r->first);
+        const int32_t first = topo.x;
+        const uint32_t meta = (uint32_t)topo.y;
+        if (meta & kLeafBit) {
+          const int32_t cnt = (int32_t)(meta & ~kLeafBit);
+          if (COUNT) scanned += (double)cnt;
+          for (int32_t k = 0; k < cnt; k++) {
+            const TgtPt* p = a.pts + first + k;
+            const double2 pxy = *reinterpret_cast<const double2*>(&p->x);
+            const double pz = p->z;
+            const double dx = pxy.x - qx;
+            const double dy = pxy.y - qy;
+            const double dz = pz - qz;
+            const double d2 = dx * dx + dy * dy + dz * dz;
+            if (d2 < best_d2) {
+              best_d2 = d2;
+              best = first + k;
+            }
+          }
+        } else {
+          const double mx = (lx + hx) / 2, my = (ly + hy) / 2, mz = (lz + hz) / 2;
+          const double ax0 = smax(0.0, smax(lx - qx, qx - mx)), ax1 = smax(0.0, smax(mx - qx, qx - hx));
+          const double ay0 = smax(0.0, smax(ly - qy, qy - my)), ay1 = smax(0.0, smax(my - qy, qy - hy));
+          const double az0 = smax(0.0, smax(lz - qz, qz - mz)), az1 = smax(0.0, smax(mz - qz, qz - hz));
+          const double sx[2] = {ax0 * ax0, ax1 * ax1};
+          const double sy[2] = {ay0 * ay0, ay1 * ay1};
+          const double sz[2] = {az0 * az0, az1 * az1};
+          const uint32_t mask = meta & 0xffu;
+          double cs[8], clo[8];
+#pragma unroll
+          for (int o = 0; o < 8; o++) {
+            cs[o] = sx[o & 1] + sy[(o >> 1) & 1] + sz[o >> 2];
+            clo[o] = cs[o] * (1.0 - 0x1p-48);
+          }
+          uint32_t rk[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+          bool hazard = false;
+#pragma unroll
+          for (int p = 0; p < 8; p++) {
+#pragma unroll
+            for (int q = p + 1; q < 8; q++) {
+              const bool both = ((mask >> p) & 1u) && ((mask >> q) & 1u);
+              const bool q_first = cs[q] < cs[p];
+              hazard |= both && q_first && !(cs[q] < clo[p]);
+              rk[p] += (both && q_first) ? 1u : 0u;
+              rk[q] += (both && !q_first) ? 1u : 0u;
+            }
+          }
+          if (hazard) {  // near-tie under sqrt: rank exactly as the reference (sqrt keys)
+            double cd[8];
+#pragma unroll
+            for (int o = 0; o < 8; o++) cd[o] = __builtin_sqrt(cs[o]);
+#pragma unroll
+            for (int o = 0; o < 8; o++) rk[o] = 0;
+#pragma unroll
+            for (int p = 0; p < 8; p++) {
+#pragma unroll
+              for (int q = p + 1; q < 8; q++) {
+                const bool both = ((mask >> p) & 1u) && ((mask >> q) & 1u);
+                const bool q_first = cd[q] < cd[p];
+                rk[p] += (both && q_first) ? 1u : 0u;
+                rk[q] += (both && !q_first) ? 1u : 0u;
+              }
+            }
+          }
+          uint32_t ranks = 0, oct0 = 0;
+#pragma unroll
+          for (int o = 0; o < 8; o++) {
+            if ((mask >> o) & 1u) {
+              const uint32_t slot = (uint32_t)__builtin_popcount(mask & ((1u << o) - 1u));
+              ranks |= slot << (3u * rk[o]);
+              if (rk[o] == 0) oct0 = (uint32_t)o;
+            }
+          }
+          const uint32_t nch = (uint32_t)__builtin_popcount(mask);
+          if (COUNT) visits += (double)nch;
+          // enter the nearest child from registers (octree.cpp:115-120 boxes)
+          node = first + (int32_t)(ranks & 7u);
+          s_node = cs[oct0];
+          if (oct0 & 1u) lx = mx; else hx = mx;
+          if (oct0 & 2u) ly = my; else hy = my;
+          if (oct0 & 4u) lz = mz; else hz = mz;
+          have_box = true;
+          descend = true;
+          if (nch > 1) {
+            st[sp * bs] = pack_entry(first, ranks >> 3, nch - 1);
+            sp++;
+            siblings_on_top = true;
+          } else {
+            siblings_on_top = false;
+          }
+        }
+      }
+      if (descend) continue;
+      if (sp == 0) break;
+      const unsigned long long e = st[(sp - 1) * bs];
+      const int32_t base = (int32_t)(uint32_t)e;
+      const uint32_t hi = (uint32_t)(e >> 32);
+      const uint32_t rem = (hi >> 24) - 1u;
+      node = base + (int32_t)(hi & 7u);
+      have_box = false;
+      if (rem == 0) {
+        sp--;
+        siblings_on_top = false;
+      } else {
+        st[(sp - 1) * bs] = pack_entry(base, (hi & 0xffffffu) >> 3, rem);
+        siblings_on_top = true;
+      }
+    }
+  }
+  nn_finish<COUNT>(a, i, active, qx, qy, qz, best, best_d2, visits, scanned, lds_stack);
+}
+
+// ---------------------------------------------------------------------------------------------
+// v3: certified fast search + exact fallback.
+//
+// Claim (the basis of the fast path): let d* = fl(d2) of the nearest target point p* and assume
+// no other point has fl(d2) <= d* (1 + 2^-48), d* in [2^-900, 2^900] and d* < init (1 - 2^-48)
+// (or d* = 0 with no other zero). Then the reference DFS returns p*, whatever its visit order:
+//  * rounding is monotone, so for a point p inside a box, fl(d2(p)) >= fl(s(box)) (same
+//    operation sequence on coordinates that are at least as far), and the reference's prune
+//    value fl(fl(sqrt(s))^2) <= s (1 + 3.0001 * 2^-53) <= d* (1 + 3.0001 * 2^-53);
+//  * so a node holding p* can only be pruned against a best within that factor of d*, i.e. by
+//    another point inside the window — there is none; p* is scanned, strict < takes it, and no
+//    later point can replace it.
+// The fast kernel therefore finds d*, p* and the second-smallest distance in ANY order — nearest
+// child first, remaining siblings in octant order, levels dropped on a 16-bit lower-bound key —
+// pruning only nodes whose s exceeds best (1 + 2^-47) (which keeps every point of the window
+// visible), and certifies each query by the window test. Queries that fail it (exact or near
+// ties, duplicates, far queries, tiny/huge distances) are appended to a list and re-run by the
+// exact reference-order DFS (k_nn_fallback). Non-finite queries are answered directly: NaN gives
+// NaN leaf distances and inf an infinite root distance, so the reference keeps index 0.
+
+constexpr double kWindow = 0x1p-48;
+constexpr double kFastPrune = 0x1p-47;
+
+__device__ __forceinline__ double box_s(double lx, double ly, double lz, double hx, double hy, double hz,
+                                        double qx, double qy, double qz) {
+  const double dx = smax(0.0, smax(lx - qx, qx - hx));
+  const double dy = smax(0.0, smax(ly - qy, qy - hy));
+  const double dz = smax(0.0, smax(lz - qz, qz - hz));
+  return dx * dx + dy * dy + dz * dz;
+}
+
+// 16-bit truncation of a non-negative double: a monotone lower bound (top 16 bits of the bits).
+__device__ __forceinline__ uint32_t key16(double v) {
+  return (uint32_t)((unsigned long long)__double_as_longlong(v) >> 48);
+}
+
+__device__ __forceinline__ bool certified(double best, double second, double init_best) {
+  if (best == 0.0) return second > 0.0;
+  return best >= 0x1p-900 && best <= 0x1p900 && second > best * (1.0 + kWindow) &&
+         best < init_best * (1.0 - kWindow);
+}
+
+// Fast-path stack entry: bits 0..31 first child record, 32..39 remaining octants,
+// 40..47 the parent's child mask, 48..63 key16 lower bound of the remaining children's s.
+template <bool APPLY>
+__global__ void __launch_bounds__(256) k_nn3(NNLaunch a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned long long lds_stack[];
+  const int bs = blockDim.x;
+  const int64_t i = (int64_t)blockIdx.x * bs + threadIdx.x;
+  const bool active = i < a.n;
+
+  double qx = 0.0, qy = 0.0, qz = 0.0;
+  nn_load_query<APPLY>(a, i, active, qx, qy, qz);
+  const bool finite_q = __builtin_isfinite(qx) && __builtin_isfinite(qy) && __builtin_isfinite(qz);
+
+  double best = __builtin_inf(), second = __builtin_inf(), thr = __builtin_inf();
+  uint32_t thr_key = key16(__builtin_inf());
+  int32_t bpos = -1;
+  if (active && finite_q) {
+    unsigned long long* st = lds_stack + threadIdx.x;
+    int sp = 0;
+    int32_t node = 0;
+    const NodeRec* r0 = a.nodes;
+    double lx = r0->lo[0], ly = r0->lo[1], lz = r0->lo[2], hx = r0->hi[0], hy = r0->hi[1], hz = r0->hi[2];
+    double s = box_s(lx, ly, lz, hx, hy, hz, qx, qy, qz);
+    while (true) {
+      bool entered = false;
+      if (!(s > thr)) {
+        const int2 topo = *reinterpret_cast<const int2*>(&a.nodes[node].first);
+        const int32_t first = topo.x;
+        const uint32_t meta = (uint32_t)topo.y;
+        if (meta & kLeafBit) {
+          const int32_t cnt = (int32_t)(meta & ~kLeafBit);
+          for (int32_t k = 0; k < cnt; k++) {
+            const TgtPt* p = a.pts + first + k;
+            const double2 pxy = *reinterpret_cast<const double2*>(&p->x);
+            const double pz = p->z;
+            const double dx = pxy.x - qx;
+            const double dy = pxy.y - qy;
+            const double dz = pz - qz;
+            const double d2 = dx * dx + dy * dy + dz * dz;
+            if (d2 < best) {
+              second = best;
+              best = d2;
+              bpos = first + k;
+              thr = best * (1.0 + kFastPrune);
+              thr_key = key16(thr);
+            } else if (d2 < second) {
+              second = d2;
+            }
+          }
+        } else {
+          const double mx = (lx + hx) / 2, my = (ly + hy) / 2, mz = (lz + hz) / 2;
+          const double ax0 = smax(0.0, smax(lx - qx, qx - mx)), ax1 = smax(0.0, smax(mx - qx, qx - hx));
+          const double ay0 = smax(0.0, smax(ly - qy, qy - my)), ay1 = smax(0.0, smax(my - qy, qy - hy));
+          const double az0 = smax(0.0, smax(lz - qz, qz - mz)), az1 = smax(0.0, smax(mz - qz, qz - hz));
+          const double sx[2] = {ax0 * ax0, ax1 * ax1};
+          const double sy[2] = {ay0 * ay0, ay1 * ay1};
+          const double sz[2] = {az0 * az0, az1 * az1};
+          const uint32_t mask = meta & 0xffu;
+          // nearest existing child (first minimum in octant order) and the smallest key of the rest
+          double bs_ = __builtin_inf();
+          uint32_t o1 = 0;
+#pragma unroll
+          for (int o = 0; o < 8; o++) {
+            const double c = sx[o & 1] + sy[(o >> 1) & 1] + sz[o >> 2];
+            const bool take = ((mask >> o) & 1u) && c < bs_;
+            bs_ = take ? c : bs_;
+            o1 = take ? (uint32_t)o : o1;
+          }
+          const uint32_t rem = mask & ~(1u << o1);
+          uint32_t kmin = 0xffffu;
+#pragma unroll
+          for (int o = 0; o < 8; o++) {
+            const double c = sx[o & 1] + sy[(o >> 1) & 1] + sz[o >> 2];
+            const uint32_t kk = key16(c);
+            kmin = ((rem >> o) & 1u) && kk < kmin ? kk : kmin;
+          }
+          if (rem) {
+            st[sp * bs] = ((unsigned long long)kmin << 48) | ((unsigned long long)mask << 40) |
+                          ((unsigned long long)rem << 32) | (uint32_t)first;
+            sp++;
+          }
+          node = first + __builtin_popcount(mask & ((1u << o1) - 1u));
+          if (o1 & 1u) lx = mx; else hx = mx;
+          if (o1 & 2u) ly = my; else hy = my;
+          if (o1 & 4u) lz = mz; else hz = mz;
+          s = bs_;
+          entered = true;
+        }
+      }
+      if (entered) continue;
+      bool found = false;
+      while (sp > 0) {
+        const unsigned long long e = st[(sp - 1) * bs];
+        if ((uint32_t)(e >> 48) > thr_key) {  // every remaining child is beyond the threshold
+          sp--;
+          continue;
+        }
+        uint32_t rem = (uint32_t)(e >> 32) & 0xffu;
+        const uint32_t pmask = (uint32_t)(e >> 40) & 0xffu;
+        const int32_t first = (int32_t)(uint32_t)e;
+        const uint32_t o = (uint32_t)__builtin_ctz(rem);
+        rem &= rem - 1u;
+        if (rem == 0) sp--;
+        else st[(sp - 1) * bs] = (e & ~(0xffull << 32)) | ((unsigned long long)rem << 32);
+        node = first + __builtin_popcount(pmask & ((1u << o) - 1u));
+        const NodeRec* r = a.nodes + node;
+        const double2 l01 = *reinterpret_cast<const double2*>(&r->lo[0]);
+        const double2 l2h0 = *reinterpret_cast<const double2*>(&r->lo[2]);
+        const double2 h12 = *reinterpret_cast<const double2*>(&r->hi[1]);
+        lx = l01.x; ly = l01.y; lz = l2h0.x; hx = l2h0.y; hy = h12.x; hz = h12.y;
+        s = box_s(lx, ly, lz, hx, hy, hz, qx, qy, qz);
+        found = true;
+        break;
+      }
+      if (!found) break;
+    }
+  }
+
+  bool ok = true;
+  int32_t pos = bpos;
+  double d = 0.0;
+  if (active) {
+    if (!finite_q) {
+      pos = a.pos0;  // findNearest keeps its default index 0 (see above)
+      const TgtPt p = a.pts[pos];
+      const double dx = qx - p.x, dy = qy - p.y, dz = qz - p.z;
+      d = __builtin_sqrt(dx * dx + dy * dy + dz * dz);
+    } else {
+      ok = certified(best, second, a.init_best);
+      d = __builtin_sqrt(best);
+    }
+    if (ok) {
+      a.pos_out[i] = pos;
+      a.dist_out[i] = d;
+    } else {
+      const unsigned slot = atomicAdd(a.fb_count, 1u);
+      a.fb_list[slot] = (int32_t)i;
+    }
+  }
+  // residual moments over the certified queries of this block (complete when the fallback list
+  // is empty; otherwise k_moments_fix recomputes every block from the final residuals)
+  if (!a.part) return;
+  __syncthreads();
+  double* red = reinterpret_cast<double*>(lds_stack);
+  const bool use = active && ok;
+  double s1[2] = {use ? 1.0 : 0.0, use ? d : 0.0};
+  block_sum<2>(s1, red);
+  const double nb = s1[0];
+  const double mean = nb > 0.0 ? s1[1] / nb : 0.0;
+  const double dev = use ? (d - mean) : 0.0;
+  const bool fin = use && __builtin_isfinite(d);
+  double s2[2] = {dev * dev, (use && !fin) ? 1.0 : 0.0};
+  block_sum<2>(s2, red);
+  double mn = fin ? d : 1.7976931348623157e308, mxv = fin ? d : 0.0;
+  block_minmax(mn, mxv, red);
+  if (threadIdx.x == 0) {
+    Moments m;
+    m.n = nb;
+    m.mean = mean;
+    m.m2 = s2[0];
+    m.dmin = mn;
+    m.dmax = mxv;
+    m.nbad = s2[1];
+    m.pad0 = 0.0;
+    m.pad1 = 0.0;
+    a.part[blockIdx.x] = m;
+  }
+}
+
+// Exact reference-order DFS for the queries the fast path could not certify.
+__global__ void __launch_bounds__(256) k_nn_fallback(NNLaunch a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned long long lds_stack[];
+  const unsigned cnt = *a.fb_count;
+  for (unsigned j = blockIdx.x * blockDim.x + threadIdx.x; j < cnt; j += gridDim.x * blockDim.x) {
+    const int64_t i = a.fb_list[j];
+    const double qx = a.x[i], qy = a.y[i], qz = a.z[i];
+    double best_d2 = a.init_best, visits = 0.0, scanned = 0.0;
+    int32_t best = -1;
+    exact_dfs<false>(a, qx, qy, qz, lds_stack + threadIdx.x, blockDim.x, best, best_d2, visits, scanned);
+    int32_t pos = best;
+    double d;
+    if (best >= 0) {
+      d = __builtin_sqrt(best_d2);
+    } else {
+      pos = a.pos0;
+      const TgtPt p = a.pts[pos];
+      const double dx = qx - p.x, dy = qy - p.y, dz = qz - p.z;
+      d = __builtin_sqrt(dx * dx + dy * dy + dz * dz);
+    }
+    a.pos_out[i] = pos;
+    a.dist_out[i] = d;
+  }
+}
+
+// When the fallback list is non-empty, rebuild every block's residual moments from the final
+// residuals (same blocks as k_nn3: deterministic whatever the list order).
+__global__ void __launch_bounds__(256) k_moments_fix(NNLaunch a) {
+  __shared__ double red[16];
+  if (*a.fb_count == 0) return;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool active = i < a.n;
+  const double d = active ? a.dist_out[i] : 0.0;
+  double s1[2] = {active ? 1.0 : 0.0, active ? d : 0.0};
+  block_sum<2>(s1, red);
+  const double nb = s1[0];
+  const double mean = s1[1] / nb;
+  const double dev = active ? (d - mean) : 0.0;
+  const bool fin = active && __builtin_isfinite(d);
+  double s2[2] = {dev * dev, (active && !fin) ? 1.0 : 0.0};
+  block_sum<2>(s2, red);
+  double mn = fin ? d : 1.7976931348623157e308, mxv = fin ? d : 0.0;
+  block_minmax(mn, mxv, red);
+  if (threadIdx.x == 0) {
+    Moments m;
+    m.n = nb;
+    m.mean = mean;
+    m.m2 = s2[0];
+    m.dmin = mn;
+    m.dmax = mxv;
+    m.nbad = s2[1];
+    m.pad0 = 0.0;
+    m.pad1 = 0.0;
+    a.part[blockIdx.x] = m;
   }
 }
 
@@ -478,12 +939,32 @@ hipError_t launch_nn(const NNLaunch& a, hipStream_t s) {
   size_t shmem = (size_t)levels * bs * sizeof(unsigned long long);
   if (shmem < 1024) shmem = 1024;  // also hosts the block reductions
   const unsigned grid = grid_for(a.n, bs);
-  if (a.apply) {
-    if (a.count) hipLaunchKernelGGL((k_nn<true, true>), dim3(grid), dim3(bs), shmem, s, a);
-    else hipLaunchKernelGGL((k_nn<true, false>), dim3(grid), dim3(bs), shmem, s, a);
+  if (a.variant == 3 && !a.count) {
+    // certified fast path -> exact fallback for the uncertified rest -> moments repair
+    if (a.apply) hipLaunchKernelGGL((k_nn3<true>), dim3(grid), dim3(bs), shmem, s, a);
+    else hipLaunchKernelGGL((k_nn3<false>), dim3(grid), dim3(bs), shmem, s, a);
+    if (a.ev_fast_done) (void)hipEventRecord(a.ev_fast_done, s);
+    const unsigned fb_grid = grid < 1024u ? grid : 1024u;
+    hipLaunchKernelGGL(k_nn_fallback, dim3(fb_grid), dim3(bs), shmem, s, a);
+    if (a.part) hipLaunchKernelGGL(k_moments_fix, dim3(grid), dim3(bs), 0, s, a);
+    return hipGetLastError();
+  }
+  if (a.variant == 1 || a.count) {
+    if (a.apply) {
+      if (a.count) hipLaunchKernelGGL((k_nn<true, true>), dim3(grid), dim3(bs), shmem, s, a);
+      else hipLaunchKernelGGL((k_nn<true, false>), dim3(grid), dim3(bs), shmem, s, a);
+    } else {
+      if (a.count) hipLaunchKernelGGL((k_nn<false, true>), dim3(grid), dim3(bs), shmem, s, a);
+      else hipLaunchKernelGGL((k_nn<false, false>), dim3(grid), dim3(bs), shmem, s, a);
+    }
   } else {
-    if (a.count) hipLaunchKernelGGL((k_nn<false, true>), dim3(grid), dim3(bs), shmem, s, a);
-    else hipLaunchKernelGGL((k_nn<false, false>), dim3(grid), dim3(bs), shmem, s, a);
+    if (a.apply) {
+      if (a.count) hipLaunchKernelGGL((k_nn2<true, true>), dim3(grid), dim3(bs), shmem, s, a);
+      else hipLaunchKernelGGL((k_nn2<true, false>), dim3(grid), dim3(bs), shmem, s, a);
+    } else {
+      if (a.count) hipLaunchKernelGGL((k_nn2<false, true>), dim3(grid), dim3(bs), shmem, s, a);
+      else hipLaunchKernelGGL((k_nn2<false, false>), dim3(grid), dim3(bs), shmem, s, a);
+    }
   }
   return hipGetLastError();
 }

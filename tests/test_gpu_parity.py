@@ -176,3 +176,44 @@ def test_empty_inputs_rejected(icp):
     assert rc != 0 and not res.success  # icpengine.cpp:31-34
     rc, res, _, _ = icp.engine_register(p, np.ones((5, 3)), np.zeros((0, 3)), device=0)
     assert rc != 0 and not res.success
+
+
+def test_kernel_variants_agree(icp, oracle):
+    """The certified fast search (default) and the literal reference-order kernels agree bit for
+    bit, including on inputs full of exact ties (lattice) where the fallback does the work."""
+    import os
+    rng = np.random.default_rng(9)
+    tgt = rng.normal(size=(200000, 3)) * [5, 5, 1]
+    q = np.concatenate([rng.normal(size=(100000, 3)) * [6, 6, 1.2], tgt[:2000]])
+    lat = np.stack(np.meshgrid(np.arange(40), np.arange(40), np.arange(10), indexing="ij"), -1).reshape(-1, 3) * 0.5
+    lq = np.concatenate([lat[rng.integers(0, len(lat), 5000)] + 0.25, rng.uniform(-1, 21, size=(5000, 3))])
+    outs = {}
+    old = os.environ.get("ICP_NN_VARIANT")
+    try:
+        for v in ("1", "2", "3"):
+            os.environ["ICP_NN_VARIANT"] = v
+            with icp.Context(0) as ctx:
+                ctx.set_target(tgt, 10, 20, icp.RULES_ENGINE)
+                a = ctx.nn(q)
+                ctx.set_target(lat.astype(float), 10, 20, icp.RULES_CLI)
+                b = ctx.nn(lq)
+            outs[v] = (a, b)
+    finally:
+        if old is None:
+            os.environ.pop("ICP_NN_VARIANT", None)
+        else:
+            os.environ["ICP_NN_VARIANT"] = old
+    for v in ("2", "3"):
+        for k in range(2):
+            np.testing.assert_array_equal(outs[v][k][0], outs["1"][k][0])
+            np.testing.assert_array_equal(outs[v][k][1], outs["1"][k][1])
+    oidx, _ = oracle.OracleTree(lat.astype(float)).nn(lq, init_best=1e20)
+    np.testing.assert_array_equal(outs["3"][1][0], oidx)
+
+
+def test_fallback_share_small_on_scans(icp, gpu_ctx):
+    tgt, src, _ = icp.synth_pair(500000)
+    gpu_ctx.set_target(tgt, 10, 20, icp.RULES_ENGINE)
+    gpu_ctx.set_source(src)
+    st = gpu_ctx.iterate(None, 0, icp.RULES_ENGINE, 3.0)
+    assert st.n_fallback <= 0.001 * len(src)
