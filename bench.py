@@ -99,7 +99,7 @@ def main() -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--n", type=int, default=10_000_000, help="points per cloud (config 4: 10M)")
+    ap.add_argument("--points", type=int, default=10_000_000, help="points per cloud (config 4: 10M)")
     ap.add_argument("--cpu-sample", type=int, default=1_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "traffic_latest.json"),
@@ -119,7 +119,7 @@ def main() -> int:
     device = local_rank % max(1, torch.cuda.device_count())  # ranks > GPUs only in rehearsals
     torch.cuda.set_device(device)
 
-    n = args.n
+    n = args.points
     t_setup = time.perf_counter()
     tgt, src, T_true = icp.synth_pair(n)
     lo, hi = shard_range(n, rank, world)
@@ -158,11 +158,12 @@ def main() -> int:
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    # untimed: how the last timed state splits over the search paths (same queries, same guess)
+    probe = ctx.iterate(None, 1, icp.RULES_ENGINE, 3.0)
     rc, res = sess.finish()
 
     # untimed: reference-DFS work of this rank's queries (the V, P of the byte model)
     v_mean, p_mean = ctx.traversal_counts()
-    probe = ctx.iterate(None, 1, icp.RULES_ENGINE, 3.0)  # untimed: fallback share of the final state
     n_local = hi - lo
     nn_avg_s = float(np.mean(nn_ms)) / 1e3
     b_corr = bytes_per_corr(v_mean, p_mean)
@@ -215,11 +216,12 @@ def main() -> int:
             "roofline": {
                 "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "kernel": "k_nn (fused transform + octree NN + residual + block moments)",
+                "kernel": "k_nn4 (fused transform + wave-cooperative certified octree NN + residual + block moments)",
                 "bytes_per_corr": round(b_corr, 1), "node_entries_per_query": round(v_mean, 3),
                 "leaf_points_per_query": round(p_mean, 3), "kernel_ms_avg": round(float(np.mean(nn_ms)), 4),
                 "iterate_device_ms_avg": round(float(np.mean(it_ms)), 4),
                 "exact_fallback_queries": int(probe.n_fallback),
+                "lane_search_queries": int(probe.n_lane_search),
             },
             "cpu_baseline": cpu,
             "setup_s": round(setup_s, 2),

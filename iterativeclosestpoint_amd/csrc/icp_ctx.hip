@@ -13,6 +13,7 @@
 #include <cfloat>
 #include <cmath>
 #include <cstdlib>
+#include <cstdio>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -21,6 +22,7 @@
 #include "icp_ctx_internal.h"
 #include "kernels.h"
 #include "octree_build.h"
+#include "query_order.h"
 
 using namespace icp;
 
@@ -128,6 +130,7 @@ void icp_hip_destroy(icp_hip_ctx* c) {
   dfree(c->counters);
   dfree(c->Tbuf);
   dfree(c->fb_count);
+  dfree(c->dbg);
   dfree(c->gm);
   dfree(c->gc);
   if (c->h_it) (void)hipHostFree(c->h_it);
@@ -187,6 +190,8 @@ int icp_hip_set_target(icp_hip_ctx* c, const double* xyz, int64_t n, int max_poi
   c->max_depth = t.max_depth;
   c->levels = t.max_inner_depth + 1 > 0 ? t.max_inner_depth + 1 : 1;
   c->init_best = (rules == ICP_RULES_CLI) ? 1e20 : DBL_MAX;  // icp_registration.cpp:201 / octree.cpp:180
+  c->have_prev = false;
+  c->have_results = false;
   return ICP_HIP_OK;
 }
 
@@ -205,54 +210,30 @@ int icp_hip_set_source(icp_hip_ctx* c, const double* xyz, int64_t n) {
   HIP_TRY(dalloc(&c->perm, n));
   HIP_TRY(dalloc(&c->pos, n));
   HIP_TRY(dalloc(&c->dist, n));
-  HIP_TRY(dalloc(&c->fb_list, n));
+  HIP_TRY(dalloc(&c->fb_list, 2 * (size_t)n));
   HIP_TRY(dalloc(&c->mparts, (size_t)(c->nb_nn + 2 * ((c->nb_nn + 255) / 256) + 4)));
   HIP_TRY(dalloc(&c->cparts, (size_t)(c->nb_cull + 2 * ((c->nb_cull + 255) / 256) + 4)));
   if (n == 0) return ICP_HIP_OK;
-  // Morton order over the source's own bounding box (host pass, then device keys + radix sort)
-  double lo[3] = {DBL_MAX, DBL_MAX, DBL_MAX}, hi[3] = {-DBL_MAX, -DBL_MAX, -DBL_MAX};
-  for (int64_t i = 0; i < n; i++)
-    for (int k = 0; k < 3; k++) {
-      const double v = xyz[3 * i + k];
-      if (std::isfinite(v)) {
-        lo[k] = v < lo[k] ? v : lo[k];
-        hi[k] = v > hi[k] ? v : hi[k];
-      }
-    }
-  double inv[3];
-  for (int k = 0; k < 3; k++) {
-    if (!(hi[k] >= lo[k])) lo[k] = hi[k] = 0.0;
-    const double ext = hi[k] - lo[k];
-    inv[k] = ext > 0.0 ? 1.0 / ext : 0.0;
+  // Spatially compact query order (kd buckets of 64 = one wave), computed on the host.
+  std::vector<int32_t> perm;
+  kd_query_order(xyz, n, 64, &perm);
+  std::vector<double> reordered((size_t)(3 * n));
+  for (int64_t k = 0; k < n; k++) {
+    const double* p = xyz + 3 * (int64_t)perm[k];
+    reordered[3 * k] = p[0];
+    reordered[3 * k + 1] = p[1];
+    reordered[3 * k + 2] = p[2];
   }
   double* aos = nullptr;
-  double *ux = nullptr, *uy = nullptr, *uz = nullptr;
-  uint64_t *keys = nullptr, *keys_sorted = nullptr;
-  int32_t* iota = nullptr;
-  void* temp = nullptr;
-  size_t temp_bytes = 0;
-  auto cleanup = [&]() {
-    dfree(aos); dfree(ux); dfree(uy); dfree(uz); dfree(keys); dfree(keys_sorted); dfree(iota);
-    if (temp) (void)hipFree(temp);
-  };
-  hipError_t e = hipSuccess;
-  if ((e = dalloc(&aos, 3 * (size_t)n)) != hipSuccess || (e = dalloc(&ux, n)) != hipSuccess ||
-      (e = dalloc(&uy, n)) != hipSuccess || (e = dalloc(&uz, n)) != hipSuccess ||
-      (e = dalloc(&keys, n)) != hipSuccess || (e = dalloc(&keys_sorted, n)) != hipSuccess ||
-      (e = dalloc(&iota, n)) != hipSuccess) {
-    cleanup();
-    return fail(ICP_HIP_ENOMEM, std::string("set_source allocation: ") + hipGetErrorString(e));
-  }
-  e = hipMemcpyAsync(aos, xyz, 3 * sizeof(double) * n, hipMemcpyHostToDevice, c->stream);
-  if (e == hipSuccess) e = launch_morton(aos, n, lo, inv, ux, uy, uz, keys, iota, c->stream);
-  if (e == hipSuccess) e = sort_pairs(nullptr, &temp_bytes, keys, keys_sorted, iota, c->perm, n, c->stream);
-  if (e == hipSuccess) e = hipMalloc(&temp, temp_bytes > 0 ? temp_bytes : 1);
-  if (e == hipSuccess) e = sort_pairs(temp, &temp_bytes, keys, keys_sorted, iota, c->perm, n, c->stream);
-  if (e == hipSuccess) e = launch_gather_soa(c->perm, ux, uy, uz, c->x, c->y, c->z, n, c->stream);
+  hipError_t e = dalloc(&aos, 3 * (size_t)n);
+  if (e == hipSuccess) e = hipMemcpyAsync(aos, reordered.data(), 3 * sizeof(double) * n, hipMemcpyHostToDevice, c->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(c->perm, perm.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, c->stream);
+  if (e == hipSuccess) e = launch_deinterleave(aos, c->x, c->y, c->z, n, c->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
-  cleanup();
+  dfree(aos);
   if (e != hipSuccess) return fail(ICP_HIP_EDEVICE, std::string("set_source: ") + hipGetErrorString(e));
   c->have_results = false;
+  c->have_prev = false;
   return ICP_HIP_OK;
 }
 
@@ -286,12 +267,19 @@ int icp_hip_iterate(icp_hip_ctx* c, const double* T_apply, int iter, int rules, 
   if (T_apply)
     for (int k = 0; k < 12; k++) a.T[k] = T_apply[k];
   a.fb_list = c->fb_list;
+  a.fb_list2 = c->fb_list + c->n_src;
   a.fb_count = c->fb_count;
-  HIP_TRY(hipMemsetAsync(c->fb_count, 0, sizeof(unsigned int), s));
+  a.have_prev = c->have_prev ? 1 : 0;
+  HIP_TRY(hipMemsetAsync(c->fb_count, 0, 2 * sizeof(unsigned int), s));
+  if (std::getenv("ICP_NN_DEBUG")) {
+    if (!c->dbg) HIP_TRY(dalloc(&c->dbg, 8));
+    HIP_TRY(hipMemsetAsync(c->dbg, 0, 8 * sizeof(unsigned long long), s));
+    a.dbg = c->dbg;
+  }
   HIP_TRY(hipEventRecord(c->ev_nn0, s));
-  a.ev_fast_done = c->nn_variant == 3 ? c->ev_nn1 : nullptr;
+  a.ev_fast_done = c->nn_variant >= 3 ? c->ev_nn1 : nullptr;
   HIP_TRY(launch_nn(a, s));
-  if (c->nn_variant != 3) HIP_TRY(hipEventRecord(c->ev_nn1, s));
+  if (c->nn_variant < 3) HIP_TRY(hipEventRecord(c->ev_nn1, s));
   HIP_TRY(launch_merge_moments(c->mparts, c->nb_nn, &c->it->m_local, s));
   const bool multi = c->nranks > 1;
   if (multi)
@@ -314,7 +302,7 @@ int icp_hip_iterate(icp_hip_ctx* c, const double* T_apply, int iter, int rules, 
     RCCL_TRY(ncclAllGather(&c->it->c_local, c->gc, sizeof(CovMoments) / sizeof(double), ncclDouble, c->comm, s));
   HIP_TRY(launch_finalize_cov(multi ? c->gc : nullptr, multi ? c->nranks : 1, c->it, s));
   HIP_TRY(hipMemcpyAsync(c->h_it, c->it, sizeof(IterDev), hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipMemcpyAsync(&c->last_fallbacks, c->fb_count, sizeof(unsigned int), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(c->last_lists, c->fb_count, 2 * sizeof(unsigned int), hipMemcpyDeviceToHost, s));
   HIP_TRY(hipEventRecord(c->ev_it1, s));
   HIP_TRY(hipStreamSynchronize(s));
   const IterDev& h = *c->h_it;
@@ -333,8 +321,20 @@ int icp_hip_iterate(icp_hip_ctx* c, const double* T_apply, int iter, int rules, 
     out->centroid_tgt[k] = h.c_global.mb[k];
   }
   for (int k = 0; k < 9; k++) out->H[k] = h.c_global.c[k];
-  out->n_fallback = c->nn_variant == 3 ? (int64_t)c->last_fallbacks : 0;
+  out->n_fallback = c->nn_variant >= 3 ? (int64_t)c->last_lists[0] : 0;
+  out->n_lane_search = c->nn_variant >= 4 ? (int64_t)c->last_lists[1] : 0;
   c->have_results = true;
+  c->have_prev = true;
+  if (c->dbg && std::getenv("ICP_NN_DEBUG")) {
+    unsigned long long h[8];
+    if (hipMemcpy(h, c->dbg, sizeof(h), hipMemcpyDeviceToHost) == hipSuccess)
+      std::fprintf(stderr,
+                   "[icp dbg] iter=%d waves=%llu overflow=%llu excluded=%llu coverage_fail=%llu not_cand=%llu "
+                   "cand_pts/wave=%.1f leaves/wave=%.1f bfs_rounds/wave=%.2f lane_list=%u fallback=%u\n",
+                   iter, h[0], h[1], h[2], h[3], h[6], h[0] ? (double)h[4] / h[0] : 0.0,
+                   h[0] ? (double)h[7] / h[0] : 0.0, h[0] ? (double)h[5] / h[0] : 0.0, c->last_lists[1],
+                   c->last_lists[0]);
+  }
   return ICP_HIP_OK;
 }
 
@@ -342,6 +342,7 @@ int icp_hip_apply(icp_hip_ctx* c, const double* T) {
   if (!c || !T) return fail(ICP_HIP_EINVAL, "null argument");
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(launch_apply(T, c->x, c->y, c->z, c->n_src, c->stream));
+  c->have_prev = false;  // queries moved without a search: previous residuals are no guess
   HIP_TRY(hipStreamSynchronize(c->stream));
   return ICP_HIP_OK;
 }
@@ -411,13 +412,14 @@ int icp_hip_nn(icp_hip_ctx* c, const double* q, int64_t n, int32_t* idx_out, dou
     a.init_best = c->init_best;
   a.variant = c->nn_variant;
     int32_t* fbl = nullptr;
-    if (e == hipSuccess) e = dalloc(&fbl, n);
+    if (e == hipSuccess) e = dalloc(&fbl, 2 * (size_t)n);
     a.fb_list = fbl;
+    a.fb_list2 = fbl + n;
     a.fb_count = c->fb_count;
-    if (e == hipSuccess) e = hipMemsetAsync(c->fb_count, 0, sizeof(unsigned int), c->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(c->fb_count, 0, 2 * sizeof(unsigned int), c->stream);
     if (e == hipSuccess) e = launch_nn(a, c->stream);
     if (e == hipSuccess)
-      e = hipMemcpyAsync(&c->last_fallbacks, c->fb_count, sizeof(unsigned int), hipMemcpyDeviceToHost, c->stream);
+      e = hipMemcpyAsync(c->last_lists, c->fb_count, 2 * sizeof(unsigned int), hipMemcpyDeviceToHost, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     dfree(fbl);
     if (e == hipSuccess) e = launch_scatter_corr(nullptr, pos, c->pts, di, d, dd, n, c->stream);

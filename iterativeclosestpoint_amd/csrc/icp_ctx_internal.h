@@ -10,7 +10,7 @@
 
 struct icp_hip_ctx {
   int device = 0;
-  int nn_variant = 3;  // search kernel variant (ICP_NN_VARIANT env, for A/B runs)
+  int nn_variant = 4;  // search kernel variant (ICP_NN_VARIANT env, for A/B runs)
   hipStream_t stream = nullptr;
   hipEvent_t ev_it0 = nullptr, ev_it1 = nullptr, ev_nn0 = nullptr, ev_nn1 = nullptr;
 
@@ -29,11 +29,13 @@ struct icp_hip_ctx {
   double* dist = nullptr;  // residual
   int32_t* fb_list = nullptr;            // queries for the exact fallback
   unsigned int* fb_count = nullptr;
-  unsigned int last_fallbacks = 0;
+  unsigned long long* dbg = nullptr;
+  unsigned int last_lists[2] = {0, 0};  // fallback / per-lane list sizes of the last search
   icp::Moments* mparts = nullptr;
   icp::CovMoments* cparts = nullptr;
   int64_t nb_nn = 0, nb_cull = 0;
   bool have_results = false;
+  bool have_prev = false;  // dist[] holds residuals of the resident queries (search guess)
 
   // per-iteration record
   icp::IterDev* it = nullptr;

@@ -500,6 +500,127 @@ __device__ __forceinline__ bool certified(double best, double second, double ini
          best < init_best * (1.0 - kWindow);
 }
 
+// Append the lanes with `want` to a list, one atomic per wave, lane order kept (the lists stay
+// in Morton order wave by wave, which keeps the follow-up searches coherent). Wave-uniform call.
+__device__ __forceinline__ void wave_append(bool want, int64_t i, unsigned* counter, int32_t* list) {
+  const unsigned long long m = __ballot(want);
+  if (m == 0) return;
+  const int lane = threadIdx.x & 63;
+  const int leader = __builtin_ctzll(m);
+  unsigned base = 0;
+  if (lane == leader) base = atomicAdd(counter, (unsigned)__popcll(m));
+  base = __shfl(base, leader, kWave);
+  const int off = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+  if (want) list[base + off] = (int32_t)i;
+}
+
+// Per-lane certified search (the fast path of one query): nearest child first, remaining
+// siblings in octant order, level drop on the 16-bit key; tracks best, second best, position.
+__device__ __forceinline__ void fast_dfs(const NNLaunch& a, double qx, double qy, double qz,
+                                         unsigned long long* st, int bs, double& best, double& second,
+                                         int32_t& bpos) {
+  double thr = __builtin_inf();
+  uint32_t thr_key = key16(__builtin_inf());
+  int sp = 0;
+  int32_t node = 0;
+  const NodeRec* r0 = a.nodes;
+  double lx = r0->lo[0], ly = r0->lo[1], lz = r0->lo[2], hx = r0->hi[0], hy = r0->hi[1], hz = r0->hi[2];
+  double s = box_s(lx, ly, lz, hx, hy, hz, qx, qy, qz);
+  while (true) {
+    bool entered = false;
+    if (!(s > thr)) {
+      const int2 topo = *reinterpret_cast<const int2*>(&a.nodes[node].first);
+      const int32_t first = topo.x;
+      const uint32_t meta = (uint32_t)topo.y;
+      if (meta & kLeafBit) {
+        const int32_t cnt = (int32_t)(meta & ~kLeafBit);
+        for (int32_t k = 0; k < cnt; k++) {
+          const TgtPt* p = a.pts + first + k;
+          const double2 pxy = *reinterpret_cast<const double2*>(&p->x);
+          const double pz = p->z;
+          const double dx = pxy.x - qx;
+          const double dy = pxy.y - qy;
+          const double dz = pz - qz;
+          const double d2 = dx * dx + dy * dy + dz * dz;
+          if (d2 < best) {
+            second = best;
+            best = d2;
+            bpos = first + k;
+            thr = best * (1.0 + kFastPrune);
+            thr_key = key16(thr);
+          } else if (d2 < second) {
+            second = d2;
+          }
+        }
+      } else {
+        const double mx = (lx + hx) / 2, my = (ly + hy) / 2, mz = (lz + hz) / 2;
+        const double ax0 = smax(0.0, smax(lx - qx, qx - mx)), ax1 = smax(0.0, smax(mx - qx, qx - hx));
+        const double ay0 = smax(0.0, smax(ly - qy, qy - my)), ay1 = smax(0.0, smax(my - qy, qy - hy));
+        const double az0 = smax(0.0, smax(lz - qz, qz - mz)), az1 = smax(0.0, smax(mz - qz, qz - hz));
+        const double sx[2] = {ax0 * ax0, ax1 * ax1};
+        const double sy[2] = {ay0 * ay0, ay1 * ay1};
+        const double sz[2] = {az0 * az0, az1 * az1};
+        const uint32_t mask = meta & 0xffu;
+        // nearest existing child (first minimum in octant order) and the smallest key of the rest
+        double bs_ = __builtin_inf();
+        uint32_t o1 = 0;
+#pragma unroll
+        for (int o = 0; o < 8; o++) {
+          const double c = sx[o & 1] + sy[(o >> 1) & 1] + sz[o >> 2];
+          const bool take = ((mask >> o) & 1u) && c < bs_;
+          bs_ = take ? c : bs_;
+          o1 = take ? (uint32_t)o : o1;
+        }
+        const uint32_t rem = mask & ~(1u << o1);
+        uint32_t kmin = 0xffffu;
+#pragma unroll
+        for (int o = 0; o < 8; o++) {
+          const double c = sx[o & 1] + sy[(o >> 1) & 1] + sz[o >> 2];
+          const uint32_t kk = key16(c);
+          kmin = ((rem >> o) & 1u) && kk < kmin ? kk : kmin;
+        }
+        if (rem) {
+          st[sp * bs] = ((unsigned long long)kmin << 48) | ((unsigned long long)mask << 40) |
+                        ((unsigned long long)rem << 32) | (uint32_t)first;
+          sp++;
+        }
+        node = first + __builtin_popcount(mask & ((1u << o1) - 1u));
+        if (o1 & 1u) lx = mx; else hx = mx;
+        if (o1 & 2u) ly = my; else hy = my;
+        if (o1 & 4u) lz = mz; else hz = mz;
+        s = bs_;
+        entered = true;
+      }
+    }
+    if (entered) continue;
+    bool found = false;
+    while (sp > 0) {
+      const unsigned long long e = st[(sp - 1) * bs];
+      if ((uint32_t)(e >> 48) > thr_key) {  // every remaining child is beyond the threshold
+        sp--;
+        continue;
+      }
+      uint32_t rem = (uint32_t)(e >> 32) & 0xffu;
+      const uint32_t pmask = (uint32_t)(e >> 40) & 0xffu;
+      const int32_t first = (int32_t)(uint32_t)e;
+      const uint32_t o = (uint32_t)__builtin_ctz(rem);
+      rem &= rem - 1u;
+      if (rem == 0) sp--;
+      else st[(sp - 1) * bs] = (e & ~(0xffull << 32)) | ((unsigned long long)rem << 32);
+      node = first + __builtin_popcount(pmask & ((1u << o) - 1u));
+      const NodeRec* r = a.nodes + node;
+      const double2 l01 = *reinterpret_cast<const double2*>(&r->lo[0]);
+      const double2 l2h0 = *reinterpret_cast<const double2*>(&r->lo[2]);
+      const double2 h12 = *reinterpret_cast<const double2*>(&r->hi[1]);
+      lx = l01.x; ly = l01.y; lz = l2h0.x; hx = l2h0.y; hy = h12.x; hz = h12.y;
+      s = box_s(lx, ly, lz, hx, hy, hz, qx, qy, qz);
+      found = true;
+      break;
+    }
+    if (!found) break;
+  }
+}
+
 // Fast-path stack entry: bits 0..31 first child record, 32..39 remaining octants,
 // 40..47 the parent's child mask, 48..63 key16 lower bound of the remaining children's s.
 template <bool APPLY>
@@ -513,111 +634,9 @@ __global__ void __launch_bounds__(256) k_nn3(NNLaunch a) {
   nn_load_query<APPLY>(a, i, active, qx, qy, qz);
   const bool finite_q = __builtin_isfinite(qx) && __builtin_isfinite(qy) && __builtin_isfinite(qz);
 
-  double best = __builtin_inf(), second = __builtin_inf(), thr = __builtin_inf();
-  uint32_t thr_key = key16(__builtin_inf());
+  double best = __builtin_inf(), second = __builtin_inf();
   int32_t bpos = -1;
-  if (active && finite_q) {
-    unsigned long long* st = lds_stack + threadIdx.x;
-    int sp = 0;
-    int32_t node = 0;
-    const NodeRec* r0 = a.nodes;
-    double lx = r0->lo[0], ly = r0->lo[1], lz = r0->lo[2], hx = r0->hi[0], hy = r0->hi[1], hz = r0->hi[2];
-    double s = box_s(lx, ly, lz, hx, hy, hz, qx, qy, qz);
-    while (true) {
-      bool entered = false;
-      if (!(s > thr)) {
-        const int2 topo = *reinterpret_cast<const int2*>(&a.nodes[node].first);
-        const int32_t first = topo.x;
-        const uint32_t meta = (uint32_t)topo.y;
-        if (meta & kLeafBit) {
-          const int32_t cnt = (int32_t)(meta & ~kLeafBit);
-          for (int32_t k = 0; k < cnt; k++) {
-            const TgtPt* p = a.pts + first + k;
-            const double2 pxy = *reinterpret_cast<const double2*>(&p->x);
-            const double pz = p->z;
-            const double dx = pxy.x - qx;
-            const double dy = pxy.y - qy;
-            const double dz = pz - qz;
-            const double d2 = dx * dx + dy * dy + dz * dz;
-            if (d2 < best) {
-              second = best;
-              best = d2;
-              bpos = first + k;
-              thr = best * (1.0 + kFastPrune);
-              thr_key = key16(thr);
-            } else if (d2 < second) {
-              second = d2;
-            }
-          }
-        } else {
-          const double mx = (lx + hx) / 2, my = (ly + hy) / 2, mz = (lz + hz) / 2;
-          const double ax0 = smax(0.0, smax(lx - qx, qx - mx)), ax1 = smax(0.0, smax(mx - qx, qx - hx));
-          const double ay0 = smax(0.0, smax(ly - qy, qy - my)), ay1 = smax(0.0, smax(my - qy, qy - hy));
-          const double az0 = smax(0.0, smax(lz - qz, qz - mz)), az1 = smax(0.0, smax(mz - qz, qz - hz));
-          const double sx[2] = {ax0 * ax0, ax1 * ax1};
-          const double sy[2] = {ay0 * ay0, ay1 * ay1};
-          const double sz[2] = {az0 * az0, az1 * az1};
-          const uint32_t mask = meta & 0xffu;
-          // nearest existing child (first minimum in octant order) and the smallest key of the rest
-          double bs_ = __builtin_inf();
-          uint32_t o1 = 0;
-#pragma unroll
-          for (int o = 0; o < 8; o++) {
-            const double c = sx[o & 1] + sy[(o >> 1) & 1] + sz[o >> 2];
-            const bool take = ((mask >> o) & 1u) && c < bs_;
-            bs_ = take ? c : bs_;
-            o1 = take ? (uint32_t)o : o1;
-          }
-          const uint32_t rem = mask & ~(1u << o1);
-          uint32_t kmin = 0xffffu;
-#pragma unroll
-          for (int o = 0; o < 8; o++) {
-            const double c = sx[o & 1] + sy[(o >> 1) & 1] + sz[o >> 2];
-            const uint32_t kk = key16(c);
-            kmin = ((rem >> o) & 1u) && kk < kmin ? kk : kmin;
-          }
-          if (rem) {
-            st[sp * bs] = ((unsigned long long)kmin << 48) | ((unsigned long long)mask << 40) |
-                          ((unsigned long long)rem << 32) | (uint32_t)first;
-            sp++;
-          }
-          node = first + __builtin_popcount(mask & ((1u << o1) - 1u));
-          if (o1 & 1u) lx = mx; else hx = mx;
-          if (o1 & 2u) ly = my; else hy = my;
-          if (o1 & 4u) lz = mz; else hz = mz;
-          s = bs_;
-          entered = true;
-        }
-      }
-      if (entered) continue;
-      bool found = false;
-      while (sp > 0) {
-        const unsigned long long e = st[(sp - 1) * bs];
-        if ((uint32_t)(e >> 48) > thr_key) {  // every remaining child is beyond the threshold
-          sp--;
-          continue;
-        }
-        uint32_t rem = (uint32_t)(e >> 32) & 0xffu;
-        const uint32_t pmask = (uint32_t)(e >> 40) & 0xffu;
-        const int32_t first = (int32_t)(uint32_t)e;
-        const uint32_t o = (uint32_t)__builtin_ctz(rem);
-        rem &= rem - 1u;
-        if (rem == 0) sp--;
-        else st[(sp - 1) * bs] = (e & ~(0xffull << 32)) | ((unsigned long long)rem << 32);
-        node = first + __builtin_popcount(pmask & ((1u << o) - 1u));
-        const NodeRec* r = a.nodes + node;
-        const double2 l01 = *reinterpret_cast<const double2*>(&r->lo[0]);
-        const double2 l2h0 = *reinterpret_cast<const double2*>(&r->lo[2]);
-        const double2 h12 = *reinterpret_cast<const double2*>(&r->hi[1]);
-        lx = l01.x; ly = l01.y; lz = l2h0.x; hx = l2h0.y; hy = h12.x; hz = h12.y;
-        s = box_s(lx, ly, lz, hx, hy, hz, qx, qy, qz);
-        found = true;
-        break;
-      }
-      if (!found) break;
-    }
-  }
-
+  if (active && finite_q) fast_dfs(a, qx, qy, qz, lds_stack + threadIdx.x, bs, best, second, bpos);
   bool ok = true;
   int32_t pos = bpos;
   double d = 0.0;
@@ -634,11 +653,9 @@ __global__ void __launch_bounds__(256) k_nn3(NNLaunch a) {
     if (ok) {
       a.pos_out[i] = pos;
       a.dist_out[i] = d;
-    } else {
-      const unsigned slot = atomicAdd(a.fb_count, 1u);
-      a.fb_list[slot] = (int32_t)i;
     }
   }
+  wave_append(active && !ok, i, a.fb_count, a.fb_list);
   // residual moments over the certified queries of this block (complete when the fallback list
   // is empty; otherwise k_moments_fix recomputes every block from the final residuals)
   if (!a.part) return;
@@ -698,7 +715,7 @@ __global__ void __launch_bounds__(256) k_nn_fallback(NNLaunch a) {
 // residuals (same blocks as k_nn3: deterministic whatever the list order).
 __global__ void __launch_bounds__(256) k_moments_fix(NNLaunch a) {
   __shared__ double red[16];
-  if (*a.fb_count == 0) return;
+  if (a.fb_count[0] == 0 && a.fb_count[1] == 0) return;
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const bool active = i < a.n;
   const double d = active ? a.dist_out[i] : 0.0;
@@ -723,6 +740,359 @@ __global__ void __launch_bounds__(256) k_moments_fix(NNLaunch a) {
     m.pad0 = 0.0;
     m.pad1 = 0.0;
     a.part[blockIdx.x] = m;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// v4: wave-cooperative certified search.
+//
+// The 64 queries of a wave are Morton neighbours. Each lane first descends (nearest child, no
+// backtracking) to a leaf and scans it: u = an actual point's fl(d2), an upper bound of its
+// nearest distance. Lanes whose radius r = sqrt(u)(1 + 2^-40) + |q| 2^-45 is below twice the
+// wave's mean radius join one search box B = bbox of [q - r, q + r]; the wave collects every leaf
+// whose box meets B by a cooperative breadth-first walk (frontier and leaf list in LDS), then
+// all lanes scan those points in lockstep (wave-uniform loop, uniform addresses). Each joined
+// lane's ball of radius r lies in B, so every point with fl(d2) <= best (1 + 2^-48) is among
+// the scanned ones and the window certificate of k_nn3 applies unchanged. Lanes that do not
+// join (outliers: far from the surface, or a wave whose candidate set overflows LDS) are queued
+// for the per-lane certified search (k_nn3_list); uncertified ones for the exact DFS.
+
+constexpr int kWaveFrontier = 256;  // node ids per frontier buffer (two buffers)
+constexpr int kWavePoints = 1024;   // candidate point positions per wave
+constexpr int kWaveLdsBytes = 2 * kWaveFrontier * 4 + kWavePoints * 4 + 64 * 32;  // + staging
+
+__device__ __forceinline__ void wave_lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, kWave);
+  return v;
+}
+__device__ __forceinline__ double wave_min_d(double v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    const double o = __shfl_xor(v, off, kWave);
+    v = o < v ? o : v;
+  }
+  return v;
+}
+__device__ __forceinline__ double wave_max_d(double v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    const double o = __shfl_xor(v, off, kWave);
+    v = o > v ? o : v;
+  }
+  return v;
+}
+__device__ __forceinline__ int wave_incl_scan(int v, int lane) {
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int t = __shfl_up(v, off, kWave);
+    if (lane >= off) v += t;
+  }
+  return v;
+}
+
+template <bool APPLY>
+__global__ void __launch_bounds__(256) k_nn4(NNLaunch a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned long long lds_stack[];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool active = i < a.n;
+  unsigned char* wl = reinterpret_cast<unsigned char*>(lds_stack) + wv * kWaveLdsBytes;
+  int32_t* fr0 = reinterpret_cast<int32_t*>(wl);
+  int32_t* fr1 = fr0 + kWaveFrontier;
+  int32_t* plist = fr1 + kWaveFrontier;                               // candidate points
+  double4* stage = reinterpret_cast<double4*>(plist + kWavePoints);   // 64 staged points
+
+  double qx = 0.0, qy = 0.0, qz = 0.0, ox = 0.0, oy = 0.0, oz = 0.0;
+  if (active) {
+    ox = a.x[i];
+    oy = a.y[i];
+    oz = a.z[i];
+  }
+  nn_load_query<APPLY>(a, i, active, qx, qy, qz);
+  const bool finite_q = __builtin_isfinite(qx) && __builtin_isfinite(qy) && __builtin_isfinite(qz);
+
+  // Phase 1: a guess u of the nearest squared distance. After an iteration on the same queries:
+  // (previous residual + displacement of the query)^2, by the triangle inequality (any guess is
+  // safe: certification below also requires best <= u). Otherwise descend (nearest child, no
+  // backtracking) to one leaf and take its smallest d2 (a true upper bound).
+  double u = __builtin_inf();
+  if (active && finite_q && a.have_prev) {
+    const double dp = a.dist_out[i];
+    const double ex = qx - ox, ey = qy - oy, ez = qz - oz;
+    const double g = dp + __builtin_sqrt(ex * ex + ey * ey + ez * ez);
+    u = (g * g) * (1.0 + 0x1p-30);
+  } else if (active && finite_q) {
+    const NodeRec* r0 = a.nodes;
+    double lx = r0->lo[0], ly = r0->lo[1], lz = r0->lo[2], hx = r0->hi[0], hy = r0->hi[1], hz = r0->hi[2];
+    int32_t node = 0;
+    while (true) {
+      const int2 topo = *reinterpret_cast<const int2*>(&a.nodes[node].first);
+      const uint32_t meta = (uint32_t)topo.y;
+      if (meta & kLeafBit) {
+        const int32_t cnt = (int32_t)(meta & ~kLeafBit);
+        for (int32_t k = 0; k < cnt; k++) {
+          const TgtPt* p = a.pts + topo.x + k;
+          const double dx = p->x - qx, dy = p->y - qy, dz = p->z - qz;
+          const double d2 = dx * dx + dy * dy + dz * dz;
+          u = d2 < u ? d2 : u;
+        }
+        break;
+      }
+      const double mx = (lx + hx) / 2, my = (ly + hy) / 2, mz = (lz + hz) / 2;
+      const double ax0 = smax(0.0, smax(lx - qx, qx - mx)), ax1 = smax(0.0, smax(mx - qx, qx - hx));
+      const double ay0 = smax(0.0, smax(ly - qy, qy - my)), ay1 = smax(0.0, smax(my - qy, qy - hy));
+      const double az0 = smax(0.0, smax(lz - qz, qz - mz)), az1 = smax(0.0, smax(mz - qz, qz - hz));
+      const double sx[2] = {ax0 * ax0, ax1 * ax1};
+      const double sy[2] = {ay0 * ay0, ay1 * ay1};
+      const double sz[2] = {az0 * az0, az1 * az1};
+      const uint32_t mask = meta & 0xffu;
+      double bs_ = __builtin_inf();
+      uint32_t o1 = 0;
+#pragma unroll
+      for (int o = 0; o < 8; o++) {
+        const double c = sx[o & 1] + sy[(o >> 1) & 1] + sz[o >> 2];
+        const bool take = ((mask >> o) & 1u) && c < bs_;
+        bs_ = take ? c : bs_;
+        o1 = take ? (uint32_t)o : o1;
+      }
+      node = topo.x + __builtin_popcount(mask & ((1u << o1) - 1u));
+      if (o1 & 1u) lx = mx; else hx = mx;
+      if (o1 & 2u) ly = my; else hy = my;
+      if (o1 & 4u) lz = mz; else hz = mz;
+    }
+  }
+
+  // Phase 2: the wave's search box over the lanes that join.
+  const bool cand = active && finite_q && u <= 0x1p900;
+  const double amax = __builtin_fmax(__builtin_fabs(qx), __builtin_fmax(__builtin_fabs(qy), __builtin_fabs(qz)));
+  const double r = cand ? __builtin_sqrt(u) * (1.0 + 0x1p-40) + amax * 0x1p-45 : 0.0;
+  const unsigned long long cmask = __ballot(cand);
+  const double mean_r = wave_sum_d(r) / (double)(cmask ? __popcll(cmask) : 1);
+  bool join = cand && r <= 2.0 * mean_r;
+  const double blx = wave_min_d(join ? qx - r : __builtin_inf());
+  const double bly = wave_min_d(join ? qy - r : __builtin_inf());
+  const double blz = wave_min_d(join ? qz - r : __builtin_inf());
+  const double bhx = wave_max_d(join ? qx + r : -__builtin_inf());
+  const double bhy = wave_max_d(join ? qy + r : -__builtin_inf());
+  const double bhz = wave_max_d(join ? qz + r : -__builtin_inf());
+
+  // Phase 3: cooperative breadth-first collection of the leaves meeting B.
+  int nleaf = 0;
+  bool overflow = false;
+  if (__ballot(join) != 0) {
+    int nf = 1;
+    int32_t* cur = fr0;
+    int32_t* nxt = fr1;
+    if (lane == 0) cur[0] = 0;
+    wave_lds_fence();
+    while (nf > 0) {
+      int nn = 0;
+      for (int base = 0; base < nf; base += 64) {
+        const int j = base + lane;
+        const bool has = j < nf;
+        // frontier nodes already meet B (tested by their parent; the root always does)
+        bool leaf = false, inner = false;
+        int32_t first = 0;
+        uint32_t meta = 0, kids = 0;
+        if (has) {
+          const NodeRec* rr = a.nodes + cur[j];
+          const int2 topo = *reinterpret_cast<const int2*>(&rr->first);
+          first = topo.x;
+          meta = (uint32_t)topo.y;
+          leaf = (meta & kLeafBit) != 0;
+          inner = !leaf;
+          if (inner) {
+            const double2 l01 = *reinterpret_cast<const double2*>(&rr->lo[0]);
+            const double2 l2h0 = *reinterpret_cast<const double2*>(&rr->lo[2]);
+            const double2 h12 = *reinterpret_cast<const double2*>(&rr->hi[1]);
+            const double lx = l01.x, ly = l01.y, lz = l2h0.x, hx = l2h0.y, hy = h12.x, hz = h12.y;
+            const double mx = (lx + hx) / 2, my = (ly + hy) / 2, mz = (lz + hz) / 2;
+            // child o spans [lo or mid, mid or hi] per axis (octree.cpp:115-120)
+            const bool x0 = lx <= bhx && mx >= blx, x1 = mx <= bhx && hx >= blx;
+            const bool y0 = ly <= bhy && my >= bly, y1 = my <= bhy && hy >= bly;
+            const bool z0 = lz <= bhz && mz >= blz, z1 = mz <= bhz && hz >= blz;
+            const uint32_t mask = meta & 0xffu;
+#pragma unroll
+            for (int o = 0; o < 8; o++) {
+              const bool hit = ((o & 1) ? x1 : x0) && ((o & 2) ? y1 : y0) && ((o & 4) ? z1 : z0);
+              kids |= (hit && ((mask >> o) & 1u)) ? (1u << o) : 0u;
+            }
+          }
+        }
+        // a leaf contributes its points (contiguous in leaf order) to the candidate list
+        const int lcnt = (has && leaf) ? (int)(meta & ~kLeafBit) : 0;
+        const int lincl = wave_incl_scan(lcnt, lane);
+        const int ltot = __shfl(lincl, 63, kWave);
+        const int lpos = nleaf + lincl - lcnt;
+        if (lcnt > 0 && lpos + lcnt <= kWavePoints)
+          for (int c = 0; c < lcnt; c++) plist[lpos + c] = first + c;
+        nleaf += ltot;
+        const int nch = __builtin_popcount(kids);
+        const int incl = wave_incl_scan(nch, lane);
+        const int tot = __shfl(incl, 63, kWave);
+        int off = nn + incl - nch;
+        if (off + nch <= kWaveFrontier) {
+          const uint32_t mask = meta & 0xffu;
+          uint32_t kk = kids;
+          while (kk) {
+            const uint32_t o = (uint32_t)__builtin_ctz(kk);
+            kk &= kk - 1u;
+            nxt[off++] = first + __builtin_popcount(mask & ((1u << o) - 1u));
+          }
+        }
+        nn += tot;
+      }
+      if (nleaf > kWavePoints || nn > kWaveFrontier) {
+        overflow = true;
+        break;
+      }
+      int32_t* t = cur;
+      cur = nxt;
+      nxt = t;
+      nf = nn;
+      if (a.dbg && lane == 0) atomicAdd(&a.dbg[5], 1ull);
+      wave_lds_fence();
+    }
+  }
+  if (overflow) join = false;
+  if (a.dbg && lane == 0) {
+    atomicAdd(&a.dbg[0], 1ull);
+    if (overflow) atomicAdd(&a.dbg[1], 1ull);
+  }
+
+  // Phase 4: every joined lane scans the candidate points in lockstep: 64 points per chunk are
+  // gathered by one load per lane (the next chunk's gather is in flight while the current one is
+  // scanned from LDS by broadcast reads).
+  double best = __builtin_inf(), second = __builtin_inf();
+  int32_t bpos = -1;
+  const int npts = nleaf;
+  if (__ballot(join) != 0 && npts > 0) {
+    wave_lds_fence();
+    double4 nxtp = make_double4(0.0, 0.0, 0.0, 0.0);
+    if (lane < npts) {
+      const int32_t g = plist[lane];
+      const TgtPt* p = a.pts + g;
+      const double2 xy = *reinterpret_cast<const double2*>(&p->x);
+      nxtp = make_double4(xy.x, xy.y, p->z, __longlong_as_double((long long)g));
+    }
+    for (int base = 0; base < npts; base += 64) {
+      wave_lds_fence();  // previous chunk's reads are done before overwriting the staging slots
+      stage[lane] = nxtp;
+      wave_lds_fence();
+      const int nb = base + 64;
+      if (nb + lane < npts) {
+        const int32_t g = plist[nb + lane];
+        const TgtPt* p = a.pts + g;
+        const double2 xy = *reinterpret_cast<const double2*>(&p->x);
+        nxtp = make_double4(xy.x, xy.y, p->z, __longlong_as_double((long long)g));
+      }
+      const int m = npts - base < 64 ? npts - base : 64;
+      for (int k = 0; k < m; k++) {
+        const double4 pt = stage[k];
+        const double dx = pt.x - qx, dy = pt.y - qy, dz = pt.z - qz;
+        const double d2 = dx * dx + dy * dy + dz * dz;
+        if (d2 < best) {
+          second = best;
+          best = d2;
+          bpos = (int32_t)__double_as_longlong(pt.w);
+        } else if (d2 < second) {
+          second = d2;
+        }
+      }
+    }
+    if (a.dbg && lane == 0) atomicAdd(&a.dbg[4], (unsigned long long)npts);
+  }
+  if (a.dbg) {
+    const unsigned long long ex = __ballot(cand && !join && !overflow);
+    const unsigned long long cov = __ballot(join && !(best <= u));
+    const unsigned long long nc = __ballot(active && finite_q && !cand);
+    if (lane == 0) {
+      atomicAdd(&a.dbg[2], (unsigned long long)__popcll(ex));
+      atomicAdd(&a.dbg[3], (unsigned long long)__popcll(cov));
+      atomicAdd(&a.dbg[6], (unsigned long long)__popcll(nc));
+      atomicAdd(&a.dbg[7], (unsigned long long)nleaf);
+    }
+  }
+
+  // Phase 5: certify, write, or queue.
+  bool written = false, to_exact = false, to_lane = false;
+  double d = 0.0;
+  int32_t pos = bpos;
+  if (active) {
+    if (!finite_q) {
+      pos = a.pos0;
+      const TgtPt p = a.pts[pos];
+      const double dx = qx - p.x, dy = qy - p.y, dz = qz - p.z;
+      d = __builtin_sqrt(dx * dx + dy * dy + dz * dz);
+      written = true;
+    } else if (join && !(best <= u)) {
+      to_lane = true;  // the guess did not cover the nearest point: search this one per lane
+    } else if (join) {
+      written = certified(best, second, a.init_best);
+      to_exact = !written;
+      d = __builtin_sqrt(best);
+    } else {
+      to_lane = true;
+    }
+    if (written) {
+      a.pos_out[i] = pos;
+      a.dist_out[i] = d;
+    }
+  }
+  wave_append(to_exact, i, a.fb_count, a.fb_list);
+  wave_append(to_lane, i, a.fb_count + 1, a.fb_list2);
+  if (!a.part) return;
+  __syncthreads();
+  double* red = reinterpret_cast<double*>(lds_stack);
+  const bool use = active && written;
+  double s1[2] = {use ? 1.0 : 0.0, use ? d : 0.0};
+  block_sum<2>(s1, red);
+  const double nb = s1[0];
+  const double mean = nb > 0.0 ? s1[1] / nb : 0.0;
+  const double dev = use ? (d - mean) : 0.0;
+  const bool fin = use && __builtin_isfinite(d);
+  double s2[2] = {dev * dev, (use && !fin) ? 1.0 : 0.0};
+  block_sum<2>(s2, red);
+  double mn = fin ? d : 1.7976931348623157e308, mxv = fin ? d : 0.0;
+  block_minmax(mn, mxv, red);
+  if (threadIdx.x == 0) {
+    Moments m;
+    m.n = nb;
+    m.mean = mean;
+    m.m2 = s2[0];
+    m.dmin = mn;
+    m.dmax = mxv;
+    m.nbad = s2[1];
+    m.pad0 = 0.0;
+    m.pad1 = 0.0;
+    a.part[blockIdx.x] = m;
+  }
+}
+
+// Per-lane certified search over the queries a wave did not take (compacted: full waves).
+__global__ void __launch_bounds__(256) k_nn3_list(NNLaunch a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned long long lds_stack[];
+  const unsigned cnt = a.fb_count[1];
+  for (unsigned j0 = blockIdx.x * blockDim.x; j0 < cnt; j0 += gridDim.x * blockDim.x) {
+    const unsigned j = j0 + threadIdx.x;
+    const bool act = j < cnt;
+    const int64_t i = act ? a.fb_list2[j] : 0;
+    bool ok = false;
+    if (act) {
+      const double qx = a.x[i], qy = a.y[i], qz = a.z[i];
+      double best = __builtin_inf(), second = __builtin_inf();
+      int32_t bpos = -1;
+      fast_dfs(a, qx, qy, qz, lds_stack + threadIdx.x, blockDim.x, best, second, bpos);
+      ok = certified(best, second, a.init_best);
+      if (ok) {
+        a.pos_out[i] = bpos;
+        a.dist_out[i] = __builtin_sqrt(best);
+      }
+    }
+    wave_append(act && !ok, i, a.fb_count, a.fb_list);
   }
 }
 
@@ -939,6 +1309,18 @@ hipError_t launch_nn(const NNLaunch& a, hipStream_t s) {
   size_t shmem = (size_t)levels * bs * sizeof(unsigned long long);
   if (shmem < 1024) shmem = 1024;  // also hosts the block reductions
   const unsigned grid = grid_for(a.n, bs);
+  if (a.variant == 4 && !a.count) {
+    // wave-cooperative search -> per-lane search for the rest -> exact fallback -> moments repair
+    const size_t shm4 = (size_t)(bs / kWave) * kWaveLdsBytes;
+    if (a.apply) hipLaunchKernelGGL((k_nn4<true>), dim3(grid), dim3(bs), shm4, s, a);
+    else hipLaunchKernelGGL((k_nn4<false>), dim3(grid), dim3(bs), shm4, s, a);
+    if (a.ev_fast_done) (void)hipEventRecord(a.ev_fast_done, s);
+    const unsigned fb_grid = grid < 1024u ? grid : 1024u;
+    hipLaunchKernelGGL(k_nn3_list, dim3(fb_grid), dim3(bs), shmem, s, a);
+    hipLaunchKernelGGL(k_nn_fallback, dim3(fb_grid), dim3(bs), shmem, s, a);
+    if (a.part) hipLaunchKernelGGL(k_moments_fix, dim3(grid), dim3(bs), 0, s, a);
+    return hipGetLastError();
+  }
   if (a.variant == 3 && !a.count) {
     // certified fast path -> exact fallback for the uncertified rest -> moments repair
     if (a.apply) hipLaunchKernelGGL((k_nn3<true>), dim3(grid), dim3(bs), shmem, s, a);

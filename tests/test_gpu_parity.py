@@ -190,7 +190,7 @@ def test_kernel_variants_agree(icp, oracle):
     outs = {}
     old = os.environ.get("ICP_NN_VARIANT")
     try:
-        for v in ("1", "2", "3"):
+        for v in ("1", "2", "3", "4"):
             os.environ["ICP_NN_VARIANT"] = v
             with icp.Context(0) as ctx:
                 ctx.set_target(tgt, 10, 20, icp.RULES_ENGINE)
@@ -203,12 +203,13 @@ def test_kernel_variants_agree(icp, oracle):
             os.environ.pop("ICP_NN_VARIANT", None)
         else:
             os.environ["ICP_NN_VARIANT"] = old
-    for v in ("2", "3"):
+    for v in ("2", "3", "4"):
         for k in range(2):
             np.testing.assert_array_equal(outs[v][k][0], outs["1"][k][0])
             np.testing.assert_array_equal(outs[v][k][1], outs["1"][k][1])
     oidx, _ = oracle.OracleTree(lat.astype(float)).nn(lq, init_best=1e20)
     np.testing.assert_array_equal(outs["3"][1][0], oidx)
+    np.testing.assert_array_equal(outs["4"][1][0], oidx)
 
 
 def test_fallback_share_small_on_scans(icp, gpu_ctx):

@@ -11,17 +11,17 @@ for v in ${1:-"1 2"}; do
              "TA_BUSY_avr TA_TA_BUSY_sum TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum"; do
     i=$((i+1))
     ICP_NN_VARIANT=$v timeout -k 10 300 rocprofv3 --pmc $set --output-format csv -d $OUT/v${v}_p$i -o p -- \
-      python3 $REPO/bench.py --n 10000000 --steps 1 --warmup 1 --no-cpu-baseline > /dev/null 2> $OUT/v${v}_p$i.err || echo "pass $i v$v rc=$?"
+      python3 $REPO/bench.py --points 10000000 --steps 1 --warmup 1 --no-cpu-baseline > /dev/null 2> $OUT/v${v}_p$i.err || echo "pass $i v$v rc=$?"
   done
 done
 cd $REPO
 python3 - <<'PY'
 import csv, glob, collections
-for v in (1, 2):
+for v in (1, 2, 3, 4):
     agg = collections.defaultdict(float); cnt = collections.defaultdict(set)
     for f in glob.glob(f"gpurun_out/sq/v{v}_p*/**/*counter_collection.csv", recursive=True):
         for r in csv.DictReader(open(f)):
-            if "k_nn" in r["Kernel_Name"] and "true, false" in r["Kernel_Name"]:
+            if "k_nn4<true>" in r["Kernel_Name"] or "k_nn3_list" in r["Kernel_Name"]:
                 agg[r["Counter_Name"]] += float(r["Counter_Value"]); cnt[r["Counter_Name"]].add(r["Dispatch_Id"])
     print(f"variant {v}:")
     for k in sorted(agg): print(f"  {k:32s} {agg[k]/max(1,len(cnt[k])):.4g}")
