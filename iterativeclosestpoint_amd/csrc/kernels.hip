@@ -969,9 +969,13 @@ __global__ void __launch_bounds__(256) k_nn4(NNLaunch a) {
   double best = __builtin_inf(), second = __builtin_inf();
   int32_t bpos = -1;
   const int npts = nleaf;
+  int scanned_pts = 0;
   if (__ballot(join) != 0 && npts > 0) {
+    // Points outside B are farther than r from every joined lane (each ball lies in B), so
+    // they can neither be a joined lane's nearest point nor sit in its certificate window.
     wave_lds_fence();
     double4 nxtp = make_double4(0.0, 0.0, 0.0, 0.0);
+    bool nin = false;
     if (lane < npts) {
       const int32_t g = plist[lane];
       const TgtPt* p = a.pts + g;
@@ -979,8 +983,12 @@ __global__ void __launch_bounds__(256) k_nn4(NNLaunch a) {
       nxtp = make_double4(xy.x, xy.y, p->z, __longlong_as_double((long long)g));
     }
     for (int base = 0; base < npts; base += 64) {
+      nin = base + lane < npts && nxtp.x >= blx && nxtp.x <= bhx && nxtp.y >= bly && nxtp.y <= bhy &&
+            nxtp.z >= blz && nxtp.z <= bhz;
+      const unsigned long long im = __ballot(nin);
+      const int slot = __builtin_amdgcn_mbcnt_hi((uint32_t)(im >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)im, 0));
       wave_lds_fence();  // previous chunk's reads are done before overwriting the staging slots
-      stage[lane] = nxtp;
+      if (nin) stage[slot] = nxtp;
       wave_lds_fence();
       const int nb = base + 64;
       if (nb + lane < npts) {
@@ -989,7 +997,8 @@ __global__ void __launch_bounds__(256) k_nn4(NNLaunch a) {
         const double2 xy = *reinterpret_cast<const double2*>(&p->x);
         nxtp = make_double4(xy.x, xy.y, p->z, __longlong_as_double((long long)g));
       }
-      const int m = npts - base < 64 ? npts - base : 64;
+      const int m = __popcll(im);
+      scanned_pts += m;
       for (int k = 0; k < m; k++) {
         const double4 pt = stage[k];
         const double dx = pt.x - qx, dy = pt.y - qy, dz = pt.z - qz;
@@ -1003,7 +1012,7 @@ __global__ void __launch_bounds__(256) k_nn4(NNLaunch a) {
         }
       }
     }
-    if (a.dbg && lane == 0) atomicAdd(&a.dbg[4], (unsigned long long)npts);
+    if (a.dbg && lane == 0) atomicAdd(&a.dbg[4], (unsigned long long)scanned_pts);
   }
   if (a.dbg) {
     const unsigned long long ex = __ballot(cand && !join && !overflow);
@@ -1130,27 +1139,46 @@ __global__ void k_finalize_moments(const Moments* gathered, int nranks, IterDev*
   it->thr = cull_threshold(mean, sd, k_sigma, iter, engine_rules);
 }
 
+constexpr int kCullPer = 4;  // queries per thread of k_cull_cov
+
 __global__ void __launch_bounds__(256) k_cull_cov(CullLaunch a) {
   __shared__ double red[4 * 9];
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const double thr = a.it->thr;
-  bool valid = false;
-  double d = 0.0, ax = 0.0, ay = 0.0, az = 0.0, bx = 0.0, by = 0.0, bz = 0.0;
-  if (i < a.n) {
-    d = a.dist[i];
-    valid = d <= thr;  // icpengine.cpp:265
-    if (valid) {
-      ax = a.x[i];
-      ay = a.y[i];
-      az = a.z[i];
-      const TgtPt* p = a.pts + a.pos[i];
-      const double2 pxy = *reinterpret_cast<const double2*>(&p->x);
-      bx = pxy.x;
-      by = pxy.y;
-      bz = p->z;
+  const int64_t base = (int64_t)blockIdx.x * (256 * kCullPer) + threadIdx.x;
+  bool valid[kCullPer];
+  double d[kCullPer], ax[kCullPer], ay[kCullPer], az[kCullPer], bx[kCullPer], by[kCullPer], bz[kCullPer];
+#pragma unroll
+  for (int e = 0; e < kCullPer; e++) {
+    const int64_t i = base + e * 256;
+    valid[e] = false;
+    d[e] = ax[e] = ay[e] = az[e] = bx[e] = by[e] = bz[e] = 0.0;
+    if (i < a.n) {
+      d[e] = a.dist[i];
+      valid[e] = d[e] <= thr;  // icpengine.cpp:265
+      if (valid[e]) {
+        ax[e] = a.x[i];
+        ay[e] = a.y[i];
+        az[e] = a.z[i];
+        const TgtPt* p = a.pts + a.pos[i];
+        const double2 pxy = *reinterpret_cast<const double2*>(&p->x);
+        bx[e] = pxy.x;
+        by[e] = pxy.y;
+        bz[e] = p->z;
+      }
     }
   }
-  double s1[8] = {valid ? 1.0 : 0.0, valid ? d * d : 0.0, ax, ay, az, bx, by, bz};
+  double s1[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+  for (int e = 0; e < kCullPer; e++) {
+    s1[0] += valid[e] ? 1.0 : 0.0;
+    s1[1] += valid[e] ? d[e] * d[e] : 0.0;
+    s1[2] += ax[e];
+    s1[3] += ay[e];
+    s1[4] += az[e];
+    s1[5] += bx[e];
+    s1[6] += by[e];
+    s1[7] += bz[e];
+  }
   block_sum<8>(s1, red);
   const double nb = s1[0];
   if (nb == 0.0) {
@@ -1159,13 +1187,18 @@ __global__ void __launch_bounds__(256) k_cull_cov(CullLaunch a) {
   }
   const double ma[3] = {s1[2] / nb, s1[3] / nb, s1[4] / nb};
   const double mb[3] = {s1[5] / nb, s1[6] / nb, s1[7] / nb};
-  const double ca[3] = {valid ? ax - ma[0] : 0.0, valid ? ay - ma[1] : 0.0, valid ? az - ma[2] : 0.0};
-  const double cb[3] = {valid ? bx - mb[0] : 0.0, valid ? by - mb[1] : 0.0, valid ? bz - mb[2] : 0.0};
-  double s2[9];
+  double s2[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
-  for (int r = 0; r < 3; r++)
+  for (int e = 0; e < kCullPer; e++) {
+    const double ca[3] = {valid[e] ? ax[e] - ma[0] : 0.0, valid[e] ? ay[e] - ma[1] : 0.0,
+                          valid[e] ? az[e] - ma[2] : 0.0};
+    const double cb[3] = {valid[e] ? bx[e] - mb[0] : 0.0, valid[e] ? by[e] - mb[1] : 0.0,
+                          valid[e] ? bz[e] - mb[2] : 0.0};
 #pragma unroll
-    for (int c = 0; c < 3; c++) s2[3 * r + c] = ca[r] * cb[c];
+    for (int r = 0; r < 3; r++)
+#pragma unroll
+      for (int c = 0; c < 3; c++) s2[3 * r + c] += ca[r] * cb[c];
+  }
   block_sum<9>(s2, red);
   if (threadIdx.x == 0) {
     CovMoments m;
@@ -1315,9 +1348,12 @@ hipError_t launch_nn(const NNLaunch& a, hipStream_t s) {
     if (a.apply) hipLaunchKernelGGL((k_nn4<true>), dim3(grid), dim3(bs), shm4, s, a);
     else hipLaunchKernelGGL((k_nn4<false>), dim3(grid), dim3(bs), shm4, s, a);
     if (a.ev_fast_done) (void)hipEventRecord(a.ev_fast_done, s);
-    const unsigned fb_grid = grid < 1024u ? grid : 1024u;
-    hipLaunchKernelGGL(k_nn3_list, dim3(fb_grid), dim3(bs), shmem, s, a);
-    hipLaunchKernelGGL(k_nn_fallback, dim3(fb_grid), dim3(bs), shmem, s, a);
+    // the lists are short: 64-thread blocks spread them over every CU (latency-bound walks)
+    const unsigned lgrid = (unsigned)((a.n + 63) / 64 < 4096 ? (a.n + 63) / 64 : 4096);
+    const size_t lshm = (size_t)levels * 64 * sizeof(unsigned long long) < 1024 ? 1024
+                        : (size_t)levels * 64 * sizeof(unsigned long long);
+    hipLaunchKernelGGL(k_nn3_list, dim3(lgrid), dim3(64), lshm, s, a);
+    hipLaunchKernelGGL(k_nn_fallback, dim3(lgrid), dim3(64), lshm, s, a);
     if (a.part) hipLaunchKernelGGL(k_moments_fix, dim3(grid), dim3(bs), 0, s, a);
     return hipGetLastError();
   }
@@ -1409,11 +1445,11 @@ hipError_t launch_finalize_moments(const Moments* gathered, int nranks, IterDev*
   return hipGetLastError();
 }
 
-int64_t cull_num_blocks(int64_t n) { return (n + 255) / 256; }
+int64_t cull_num_blocks(int64_t n) { return (n + 256 * kCullPer - 1) / (256 * kCullPer); }
 
 hipError_t launch_cull_cov(const CullLaunch& a, hipStream_t s) {
   if (a.n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_cull_cov, dim3(grid_for(a.n, 256)), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_cull_cov, dim3((unsigned)cull_num_blocks(a.n)), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 
