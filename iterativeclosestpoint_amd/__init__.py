@@ -1,7 +1,7 @@
 """iterativeclosestpoint_amd — MI355X-native ICP correspondence-and-alignment path.
 
 The product is the C-ABI shared library ``libicp_hip.so`` (HIP kernels for gfx950 + C++ host
-driver, declared in ``include/icp_hip.h``, ``include/icp_engine.h``, ``include/icp_host.h``).
+driver, declared in ``include/icp_hip.h``, ``include/icp_engine.h``, ``include/icp_host.h``, ``include/icp_las.h``).
 This package is only the Python harness binding of that library (ctypes), used by the tests
 and ``bench.py``. There is no CPU fallback: if the library is missing the import of
 ``lib()`` raises, and every device call fails loudly when no GPU is present.
@@ -25,6 +25,12 @@ from ._lib import (  # noqa: F401
     cov_from_pairs,
     cov_merge,
     cull_threshold,
+    las_read,
+    las_write_core,
+    las_write_cli,
+    write_transform_report,
+    LAS_CORE,
+    LAS_CLI,
     RULES_ENGINE,
     RULES_CLI,
     FLAG_NO_EARLY_STOP,

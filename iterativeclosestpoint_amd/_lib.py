@@ -89,6 +89,13 @@ class OctreeInfo(C.Structure):
     ]
 
 
+class LasHeader(C.Structure):
+    _fields_ = [
+        ("offset_to_points", C.c_uint32), ("num_points", C.c_uint32), ("record_length", C.c_uint16),
+        ("scale", C.c_double * 3), ("offset", C.c_double * 3), ("max", C.c_double * 3), ("min", C.c_double * 3),
+    ]
+
+
 class SynthSpec(C.Structure):
     _fields_ = [
         ("sigma", C.c_double * 3), ("yaw_deg", C.c_double), ("pitch_deg", C.c_double),
@@ -148,6 +155,12 @@ SIGNATURES = {
     "icp_cull_threshold": (C.c_double, [C.c_double, C.c_double, C.c_double, C.c_int, C.c_int]),
     "icp_synth_default": (None, [C.POINTER(SynthSpec)]),
     "icp_synth_pair": (C.c_int, [C.POINTER(SynthSpec), C.c_int64, C.c_int64, _P, _P, _P]),
+    # icp_las.h
+    "icp_las_read_header": (C.c_int, [C.c_char_p, C.c_int, C.POINTER(LasHeader)]),
+    "icp_las_read": (C.c_int64, [C.c_char_p, C.c_int, C.c_int64, _P, C.POINTER(LasHeader)]),
+    "icp_las_write_core": (C.c_int, [C.c_char_p, _P, C.c_int64]),
+    "icp_las_write_cli": (C.c_int, [C.c_char_p, _P, C.c_int64, _P, _P]),
+    "icp_write_transform_report": (C.c_int, [C.c_char_p, _P, _P, _P, C.c_int32]),
 }
 
 _LIB = None
@@ -475,3 +488,51 @@ def cov_merge(parts):
 
 def cull_threshold(mean, sd, k_sigma, iteration, engine_rules):
     return lib().icp_cull_threshold(mean, sd, k_sigma, iteration, engine_rules)
+
+
+LAS_CORE = 0
+LAS_CLI = 1
+
+
+def las_read(path, rules=LAS_CLI, max_points=0):
+    """Read a LAS 1.2 file (core LASIO::readLAS or CLI readLASFile rules). Returns (xyz, header)."""
+    hdr = LasHeader()
+    bpath = str(path).encode()
+    rc = lib().icp_las_read_header(bpath, rules, C.byref(hdr))
+    if rc != 0:
+        raise IcpError(rc, f"cannot read LAS header of {path}")
+    n = hdr.num_points if max_points <= 0 or rules == LAS_CLI else min(hdr.num_points, max_points)
+    xyz = np.empty((max(n, 1), 3))
+    got = lib().icp_las_read(bpath, rules, max_points, _ptr(xyz), C.byref(hdr))
+    if got < 0:
+        raise IcpError(int(got), f"cannot read LAS points of {path}")
+    return xyz[:got], hdr
+
+
+def las_write_core(path, xyz):
+    xyz = _aos(xyz)
+    rc = lib().icp_las_write_core(str(path).encode(), _ptr(xyz), xyz.shape[0])
+    if rc != 0:
+        raise IcpError(rc, f"cannot write {path}")
+
+
+def las_write_cli(path, xyz, scale=(0.001, 0.001, 0.001), offset=(0.0, 0.0, 0.0)):
+    xyz = _aos(xyz)
+    sc = np.ascontiguousarray(scale, np.float64)
+    of = np.ascontiguousarray(offset, np.float64)
+    rc = lib().icp_las_write_cli(str(path).encode(), _ptr(xyz), xyz.shape[0], _ptr(sc), _ptr(of))
+    if rc != 0:
+        raise IcpError(rc, f"cannot write {path}")
+
+
+def write_transform_report(path, R, t, transforms=None):
+    R = np.ascontiguousarray(R, np.float64).reshape(9)
+    t = np.ascontiguousarray(t, np.float64).reshape(3)
+    if transforms is None or len(transforms) == 0:
+        T, n = None, 0
+    else:
+        T = np.ascontiguousarray(transforms, np.float64).reshape(-1, 16)
+        n = T.shape[0]
+    rc = lib().icp_write_transform_report(str(path).encode(), _ptr(R), _ptr(t), _ptr(T), n)
+    if rc != 0:
+        raise IcpError(rc, f"cannot write {path}")

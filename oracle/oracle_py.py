@@ -244,3 +244,31 @@ def ref_mat4_mul(A, B):
     Cm = np.empty(16)
     reference().ref_mat4_mul(_p(A), _p(B), _p(Cm))
     return Cm.reshape(4, 4)
+
+
+def ref_read_las(path, cap=10_000_000):
+    L = reference()
+    L.ref_read_las.restype = C.c_int64
+    L.ref_read_las.argtypes = [C.c_char_p, _P, C.c_int64, _P]
+    xyz = np.empty((cap, 3))
+    so = np.empty(6)
+    n = L.ref_read_las(str(path).encode(), _p(xyz), cap, _p(so))
+    return (None, None) if n < 0 else (xyz[:n].copy(), so)
+
+
+def ref_save_las(path, xyz, scale, offset):
+    L = reference()
+    L.ref_save_las.argtypes = [C.c_char_p, _P, C.c_int64, _P, _P]
+    xyz = _aos(xyz)
+    sc = np.ascontiguousarray(scale, np.float64)
+    of = np.ascontiguousarray(offset, np.float64)
+    L.ref_save_las(str(path).encode(), _p(xyz), xyz.shape[0], _p(sc), _p(of))
+
+
+def ref_save_transformation(path, R, t, transforms):
+    L = reference()
+    L.ref_save_transformation.argtypes = [C.c_char_p, _P, _P, _P, C.c_int]
+    R = np.ascontiguousarray(R, np.float64).reshape(9)
+    t = np.ascontiguousarray(t, np.float64).reshape(3)
+    T = np.ascontiguousarray(transforms, np.float64).reshape(-1, 16)
+    L.ref_save_transformation(str(path).encode(), _p(R), _p(t), _p(T), T.shape[0])

@@ -144,3 +144,61 @@ void ref_mat4_mul(const double A16[16], const double B16[16], double C16[16]) {
 }
 
 }  // extern "C"
+
+extern "C" {
+
+// readLASFile (icp_registration.cpp:248-378). Returns the number of points (<= cap copied),
+// -1 on failure; scale/offset of the file in so[6].
+int64_t ref_read_las(const char* path, double* xyz, int64_t cap, double so[6]) {
+  PointCloud c;
+  std::streambuf* old = std::cout.rdbuf();
+  std::ofstream devnull("/dev/null");
+  std::cout.rdbuf(devnull.rdbuf());
+  bool ok = readLASFile(path, c);
+  std::cout.rdbuf(old);
+  if (!ok) return -1;
+  for (int64_t i = 0; i < (int64_t)c.points.size() && i < cap; i++) {
+    xyz[3 * i] = c.points[i].x;
+    xyz[3 * i + 1] = c.points[i].y;
+    xyz[3 * i + 2] = c.points[i].z;
+  }
+  so[0] = c.x_scale; so[1] = c.y_scale; so[2] = c.z_scale;
+  so[3] = c.x_offset; so[4] = c.y_offset; so[5] = c.z_offset;
+  return (int64_t)c.points.size();
+}
+
+// saveResultAsLAS (icp_registration.cpp:698-815) with the given scale/offset.
+void ref_save_las(const char* path, const double* xyz, int64_t n, const double scale[3], const double offset[3]) {
+  PointCloud c;
+  c.x_scale = scale[0]; c.y_scale = scale[1]; c.z_scale = scale[2];
+  c.x_offset = offset[0]; c.y_offset = offset[1]; c.z_offset = offset[2];
+  for (int64_t i = 0; i < n; i++) c.addPoint(Point3D(xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2]));
+  std::streambuf* old = std::cout.rdbuf();
+  std::ofstream devnull("/dev/null");
+  std::cout.rdbuf(devnull.rdbuf());
+  saveResultAsLAS(c, path);
+  std::cout.rdbuf(old);
+}
+
+// saveTransformation (icp_registration.cpp:625-695).
+void ref_save_transformation(const char* path, const double R9[9], const double t3[3], const double* T16, int n) {
+  double R[3][3], t[3];
+  for (int i = 0; i < 3; i++) {
+    for (int j = 0; j < 3; j++) R[i][j] = R9[3 * i + j];
+    t[i] = t3[i];
+  }
+  std::vector<Eigen::Matrix4d> hist;
+  for (int k = 0; k < n; k++) {
+    Eigen::Matrix4d M;
+    for (int r = 0; r < 4; r++)
+      for (int c = 0; c < 4; c++) M(r, c) = T16[16 * k + 4 * r + c];
+    hist.push_back(M);
+  }
+  std::streambuf* old = std::cout.rdbuf();
+  std::ofstream devnull("/dev/null");
+  std::cout.rdbuf(devnull.rdbuf());
+  saveTransformation(R, t, path, n > 0 ? &hist : nullptr);
+  std::cout.rdbuf(old);
+}
+
+}  // extern "C"

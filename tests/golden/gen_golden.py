@@ -178,15 +178,72 @@ def nn_100k_hashes():
             "mean_leaf_points": scanned / len(src)}
 
 
+def las_and_report():
+    """(f1) LAS 1.2 writer/reader and the transformation report of the reference CLI.
+
+    saveResultAsLAS / readLASFile / saveTransformation (icp_registration.cpp:625-815, :248-378),
+    run by the compiled reference. The core LASIO (core/lasio.cpp) includes Qt headers via
+    pointcloud.h and is unbuildable here: its reader shares this arithmetic, its writer is
+    restated only (tests/test_las.py says so)."""
+    import tempfile
+    rng = np.random.default_rng(77)
+    n = 12345  # > one 10000-record batch, ragged tail
+    xyz = np.stack([rng.normal(0, 30, n) - 5.0, rng.normal(0, 20, n) + 7.0, rng.normal(0, 3, n)], 1)
+    xyz[:4] = [[0.0, 0.0, 0.0], [-0.0049999, 0.0049999, -1e-9], [-123.4567891, 98.7654321, -0.0051], [1e3, -1e3, 5.0]]
+    scale = np.array([0.01, 0.01, 0.005])
+    offset = np.array([100.0, -50.0, 3.0])
+    arrays = {"las_points": xyz, "las_scale": scale, "las_offset": offset}
+    with tempfile.TemporaryDirectory() as d:
+        f = Path(d) / "w.las"
+        O.ref_save_las(f, xyz, scale, offset)
+        blob = f.read_bytes()
+        arrays["las_file"] = np.frombuffer(blob, np.uint8)
+        rd, so = O.ref_read_las(f)
+        arrays["las_read"] = rd
+        arrays["las_read_so"] = so
+        # truncated file: header claims n points, data stops mid-record in the second batch
+        cut = 227 + 20 * 10007 + 7
+        (Path(d) / "t.las").write_bytes(blob[:cut])
+        rt, _ = O.ref_read_las(Path(d) / "t.las")
+        arrays["las_trunc_cut"] = np.array([cut])
+        arrays["las_trunc_read"] = rt
+        # the reference rejects 0 points (readLASFile :291)
+        z = bytearray(blob[:227])
+        z[107:111] = (0).to_bytes(4, "little")
+        (Path(d) / "z.las").write_bytes(bytes(z))
+        rz, _ = O.ref_read_las(Path(d) / "z.las")
+        arrays["las_zero_rejected"] = np.array([rz is None])
+        # transformation report: with and without the per-iteration list
+        R = np.array([[0.9961946981, -0.0871557427, 0.0], [0.0871557427, 0.9961946981, 0.0], [0.0, 0.0, 1.0]])
+        R = R + rng.normal(0, 1e-7, (3, 3))
+        t = np.array([0.5, -0.3, 1.0 / 3.0])
+        Ts = np.stack([np.eye(4) + rng.normal(0, 1e-3, (4, 4)) for _ in range(3)])
+        Ts[:, 3] = [0, 0, 0, 1]
+        arrays["rep_R"], arrays["rep_t"], arrays["rep_T"] = R, t, Ts
+        O.ref_save_transformation(Path(d) / "r1.txt", R, t, Ts)
+        O.ref_save_transformation(Path(d) / "r0.txt", R, t, np.zeros((0, 16)))
+        arrays["rep_with_iters"] = np.frombuffer((Path(d) / "r1.txt").read_bytes(), np.uint8)
+        arrays["rep_final_only"] = np.frombuffer((Path(d) / "r0.txt").read_bytes(), np.uint8)
+    np.savez_compressed(OUT / "las_report.npz", **arrays)
+    return {"n": n, "file_bytes": len(blob), "file_fnv1a": fnv1a(arrays["las_file"]), "trunc_cut": cut}
+
+
 def main():
     if not O.reference_available():
         O.build(ref=True)
+    if "--only-las" in sys.argv:
+        meta = json.loads((OUT / "golden.json").read_text())
+        meta["las_report"] = las_and_report()
+        (OUT / "golden.json").write_text(json.dumps(meta, indent=1, sort_keys=True))
+        print(json.dumps(meta["las_report"], indent=1))
+        return
     meta = {"generator": "tests/golden/gen_golden.py", "reference": "icp_registration.cpp + vendored Eigen 3.3.4 "
             "(oracle/_ref/libicp_ref.so, g++ -O2 -ffp-contract=off, no -march)"}
     meta["nn_known_answers"] = nn_known_answers()
     meta["svd_transform"] = svd_and_transform()
     meta["icp_cli"] = icp_cli_cases()
     meta["nn_100k"] = nn_100k_hashes()
+    meta["las_report"] = las_and_report()
     (OUT / "golden.json").write_text(json.dumps(meta, indent=1, sort_keys=True))
     print(json.dumps(meta, indent=1))
 

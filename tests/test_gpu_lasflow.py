@@ -1,0 +1,111 @@
+"""End-to-end LAS flows on the GPU (BASELINE configs[2]).
+
+* the standalone CLI binary (icp_registration.cpp:817-949 rebuilt as bin/icp_registration) on a
+  LAS pair: its outputs are checked against the oracle's CLI ICP() (oracle pinned to the
+  reference by tests/test_oracle_golden.py) and the reference-pinned LAS writer/report;
+* config 3: a 1M<->1M pair written and read through the core LASIO rules, 50 engine iterations
+  with the 3-sigma cull, compared with the oracle on a 100k stride sample of the same flow and
+  with the known motion at full size.
+"""
+from __future__ import annotations
+
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from iterativeclosestpoint_amd import _lib
+
+pytestmark = pytest.mark.gpu
+
+CLI = _lib.PKG_DIR / "bin" / "icp_registration"
+SCALE = np.array([0.001, 0.001, 0.001])
+OFFSET = np.array([512.0, -256.0, 10.0])
+
+
+def _nums(text):
+    return np.array([float(x) for x in re.findall(r"-?\d+(?:\.\d+)?(?:e[-+]?\d+)?", text)])
+
+
+def test_cli_binary_matches_oracle(icp, oracle, tmp_path):
+    assert CLI.exists(), "bin/icp_registration not built (make -C iterativeclosestpoint_amd/csrc)"
+    tgt, src, _ = icp.synth_pair(120000, yaw_deg=4.0, sigma=(6.0, 3.0, 1.0))
+    tgt, src = tgt + [500.0, -250.0, 12.0], src + [500.0, -250.0, 12.0]
+    _lib.las_write_cli(tmp_path / "s.las", src, SCALE, OFFSET)
+    _lib.las_write_cli(tmp_path / "t.las", tgt, SCALE, OFFSET)
+    r = subprocess.run([str(CLI), "--source", str(tmp_path / "s.las"), "--target", str(tmp_path / "t.las"),
+                        "--sample-rate", "6", "--outdir", str(tmp_path)], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+
+    # the same flow on the CPU oracle: read (pinned reader), stride 6, CLI ICP(20, 1e-2)
+    s_in, _ = _lib.las_read(tmp_path / "s.las")
+    t_in, _ = _lib.las_read(tmp_path / "t.las")
+    ss, ts = s_in[::6], t_in[::6]
+    rc, res, hist, s_out = oracle.icp(ss, ts, oracle.SEM_CLI, 20, 1e-2)
+    assert rc == 0
+
+    sampled, _ = _lib.las_read(tmp_path / "sampled_source.las")
+    assert sampled.tobytes() == _lib.las_read(_write(tmp_path / "x.las", ss))[0].tobytes()
+    reg, _ = _lib.las_read(tmp_path / "registered_source.las")
+    ref_reg, _ = _lib.las_read(_write(tmp_path / "y.las", s_out))
+    assert reg.shape == ref_reg.shape
+    assert np.max(np.abs(reg - ref_reg)) <= 0.001 + 1e-9  # one LSB at most (truncation boundary)
+    assert np.mean(reg == ref_reg) > 0.999
+    tgt_out, _ = _lib.las_read(tmp_path / "registered_target.las")
+    assert tgt_out.tobytes() == _lib.las_read(_write(tmp_path / "z.las", ts))[0].tobytes()
+
+    # the binary's report and registered cloud are exactly what the library call writes ...
+    R, t, trs, s_gpu = icp.cli_icp(ss, ts, 20, 1e-2, device=0)
+    _lib.write_transform_report(tmp_path / "lib_report.txt", R, t, trs)
+    assert (tmp_path / "icp_transformation.txt").read_bytes() == (tmp_path / "lib_report.txt").read_bytes()
+    assert reg.tobytes() == _lib.las_read(_write(tmp_path / "w.las", s_gpu))[0].tobytes()
+    # ... and agree with the oracle's CLI ICP()
+    ref_tr = np.array([np.array(h.T_cum).reshape(4, 4) for h in hist if h.has_transform])
+    assert trs.shape == ref_tr.shape
+    np.testing.assert_allclose(trs, ref_tr, atol=1e-9)
+    np.testing.assert_allclose(R.reshape(9), np.array(res.final_R), atol=1e-9)
+    np.testing.assert_allclose(t, np.array(res.final_t), atol=1e-9)
+    rows = [_nums(line) for line in (tmp_path / "icp_transformation.txt").read_text().splitlines()
+            if line.startswith("  [")]
+    assert len(rows) == 4 * len(trs) + 3 + 1 + 4
+
+
+def _write(path, xyz):
+    _lib.las_write_cli(path, xyz, SCALE, OFFSET)
+    return path
+
+
+def _Tres(res):
+    T = np.eye(4)
+    T[:3, :3] = np.array(res.final_R).reshape(3, 3)
+    T[:3, 3] = res.final_t
+    return T
+
+
+def test_config3_las_pair_engine_50_iterations(icp, oracle, tmp_path):
+    """configs[2]: 1M<->1M pair through LASIO::writeLAS/readLAS rules, 3-sigma cull on, 50 iters."""
+    tgt, src, T_true = icp.synth_pair(1_000_000, sigma=[8.0, 4.0, 1.5], yaw_deg=1.0, pitch_deg=0.5,
+                                      roll_deg=-0.3, t=[0.05, -0.03, 0.02])
+    _lib.las_write_core(tmp_path / "src.las", src)
+    _lib.las_write_core(tmp_path / "tgt.las", tgt)
+    s_in, hs = _lib.las_read(tmp_path / "src.las", _lib.LAS_CORE)
+    t_in, _ = _lib.las_read(tmp_path / "tgt.las", _lib.LAS_CORE)
+    assert s_in.shape == src.shape and hs.num_points == len(src)
+    assert np.max(np.abs(s_in - src)) <= 0.001 * (1 + 1e-9)
+    p = icp.params_default(max_iterations=50)
+    rc, res, hist, _ = icp.engine_register(p, s_in, t_in, device=0)
+    assert rc == 0 and res.success
+    assert all(h.outlier_points > 0 for h in hist[1:])  # the cull is active (1% outliers injected)
+    T = _Tres(res)
+    np.testing.assert_allclose(T[:3, :3], T_true[:3, :3], atol=2e-4)
+    np.testing.assert_allclose(T[:3, 3], T_true[:3, 3], atol=2e-3)
+    # the same flow on a 100k stride sample against the oracle (engine rules)
+    ss, ts = s_in[::10], t_in[::10]
+    rc, res_g, hist_g, _ = icp.engine_register(p, ss, ts, device=0)
+    orc, ores, ohist, _ = oracle.icp(ss, ts, oracle.SEM_ENGINE, 50, p.tolerance)
+    assert rc == 0 and orc == 0
+    assert res_g.total_iterations == ores.total_iterations
+    assert [h.valid_points for h in hist_g] == [h.valid for h in ohist]
+    np.testing.assert_allclose(_Tres(res_g), _Tres(ores), atol=1e-10)
