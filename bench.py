@@ -222,6 +222,7 @@ def main() -> int:
                 "iterate_device_ms_avg": round(float(np.mean(it_ms)), 4),
                 "exact_fallback_queries": int(probe.n_fallback),
                 "lane_search_queries": int(probe.n_lane_search),
+                "ball_search_queries": int(probe.n_ball_search),
             },
             "cpu_baseline": cpu,
             "setup_s": round(setup_s, 2),

@@ -63,8 +63,10 @@ typedef struct icp_iter_stats {
   double H[9];        /* sum (a-ca)(b-cb)^T row-major        icpengine.cpp:86-90  */
   int64_t n_fallback; /* this rank's queries the certified fast search handed to the exact
                          reference-order DFS (near-ties)                     */
-  int64_t n_lane_search; /* this rank's queries the wave-cooperative search left to the
-                            per-lane certified search (outliers, overflowing waves)          */
+  int64_t n_lane_search; /* this rank's queries left to the per-lane certified search (no
+                            usable distance guess, or an overflowing one-query ball search)  */
+  int64_t n_ball_search; /* this rank's queries a wave did not take (outliers, overflowing
+                            waves), searched one query per wave around their guess            */
 } icp_iter_stats;
 
 int icp_hip_device_count(int* count);

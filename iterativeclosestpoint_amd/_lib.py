@@ -33,7 +33,7 @@ class IterStats(C.Structure):
         ("valid", C.c_int64), ("rmse", C.c_double), ("sum_d2", C.c_double), ("min_d", C.c_double),
         ("max_d", C.c_double), ("n_bad", C.c_int64), ("centroid_src", C.c_double * 3),
         ("centroid_tgt", C.c_double * 3), ("H", C.c_double * 9), ("n_fallback", C.c_int64),
-        ("n_lane_search", C.c_int64),
+        ("n_lane_search", C.c_int64), ("n_ball_search", C.c_int64),
     ]
 
     def as_dict(self) -> dict:

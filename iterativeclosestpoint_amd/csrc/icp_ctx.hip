@@ -73,6 +73,7 @@ static void free_source(icp_hip_ctx* c) {
   dfree(c->pos);
   dfree(c->dist);
   dfree(c->fb_list);
+  dfree(c->fb_u);
   dfree(c->mparts);
   dfree(c->cparts);
   c->n_src = 0;
@@ -111,7 +112,7 @@ int icp_hip_create(icp_hip_ctx** out, int device) {
   for (hipEvent_t* ev : {&c->ev_it0, &c->ev_it1, &c->ev_nn0, &c->ev_nn1}) (void)hipEventCreate(ev);
   if (dalloc(&c->it, 1) != hipSuccess || hipHostMalloc(reinterpret_cast<void**>(&c->h_it), sizeof(IterDev)) != hipSuccess ||
       dalloc(&c->counters, 2) != hipSuccess || dalloc(&c->Tbuf, 16) != hipSuccess ||
-      dalloc(&c->fb_count, 2) != hipSuccess) {
+      dalloc(&c->fb_count, 3) != hipSuccess) {
     icp_hip_destroy(c);
     return fail(ICP_HIP_ENOMEM, "context allocation failed");
   }
@@ -210,7 +211,8 @@ int icp_hip_set_source(icp_hip_ctx* c, const double* xyz, int64_t n) {
   HIP_TRY(dalloc(&c->perm, n));
   HIP_TRY(dalloc(&c->pos, n));
   HIP_TRY(dalloc(&c->dist, n));
-  HIP_TRY(dalloc(&c->fb_list, 2 * (size_t)n));
+  HIP_TRY(dalloc(&c->fb_list, 3 * (size_t)n));
+  HIP_TRY(dalloc(&c->fb_u, (size_t)n));
   HIP_TRY(dalloc(&c->mparts, (size_t)(c->nb_nn + 2 * ((c->nb_nn + 255) / 256) + 4)));
   HIP_TRY(dalloc(&c->cparts, (size_t)(c->nb_cull + 2 * ((c->nb_cull + 255) / 256) + 4)));
   if (n == 0) return ICP_HIP_OK;
@@ -268,12 +270,14 @@ int icp_hip_iterate(icp_hip_ctx* c, const double* T_apply, int iter, int rules, 
     for (int k = 0; k < 12; k++) a.T[k] = T_apply[k];
   a.fb_list = c->fb_list;
   a.fb_list2 = c->fb_list + c->n_src;
+  a.fb_list3 = c->fb_list + 2 * c->n_src;
+  a.fb_u2 = c->fb_u;
   a.fb_count = c->fb_count;
   a.have_prev = c->have_prev ? 1 : 0;
-  HIP_TRY(hipMemsetAsync(c->fb_count, 0, 2 * sizeof(unsigned int), s));
+  HIP_TRY(hipMemsetAsync(c->fb_count, 0, 3 * sizeof(unsigned int), s));
   if (std::getenv("ICP_NN_DEBUG")) {
-    if (!c->dbg) HIP_TRY(dalloc(&c->dbg, 8));
-    HIP_TRY(hipMemsetAsync(c->dbg, 0, 8 * sizeof(unsigned long long), s));
+    if (!c->dbg) HIP_TRY(dalloc(&c->dbg, 16));
+    HIP_TRY(hipMemsetAsync(c->dbg, 0, 16 * sizeof(unsigned long long), s));
     a.dbg = c->dbg;
   }
   HIP_TRY(hipEventRecord(c->ev_nn0, s));
@@ -302,7 +306,7 @@ int icp_hip_iterate(icp_hip_ctx* c, const double* T_apply, int iter, int rules, 
     RCCL_TRY(ncclAllGather(&c->it->c_local, c->gc, sizeof(CovMoments) / sizeof(double), ncclDouble, c->comm, s));
   HIP_TRY(launch_finalize_cov(multi ? c->gc : nullptr, multi ? c->nranks : 1, c->it, s));
   HIP_TRY(hipMemcpyAsync(c->h_it, c->it, sizeof(IterDev), hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipMemcpyAsync(c->last_lists, c->fb_count, 2 * sizeof(unsigned int), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(c->last_lists, c->fb_count, 3 * sizeof(unsigned int), hipMemcpyDeviceToHost, s));
   HIP_TRY(hipEventRecord(c->ev_it1, s));
   HIP_TRY(hipStreamSynchronize(s));
   const IterDev& h = *c->h_it;
@@ -322,18 +326,28 @@ int icp_hip_iterate(icp_hip_ctx* c, const double* T_apply, int iter, int rules, 
   }
   for (int k = 0; k < 9; k++) out->H[k] = h.c_global.c[k];
   out->n_fallback = c->nn_variant >= 3 ? (int64_t)c->last_lists[0] : 0;
-  out->n_lane_search = c->nn_variant >= 4 ? (int64_t)c->last_lists[1] : 0;
+  out->n_lane_search = c->nn_variant >= 4 ? (int64_t)c->last_lists[2] : 0;
+  out->n_ball_search = c->nn_variant >= 4 ? (int64_t)c->last_lists[1] : 0;
   c->have_results = true;
   c->have_prev = true;
   if (c->dbg && std::getenv("ICP_NN_DEBUG")) {
-    unsigned long long h[8];
-    if (hipMemcpy(h, c->dbg, sizeof(h), hipMemcpyDeviceToHost) == hipSuccess)
+    unsigned long long h[16];
+    if (hipMemcpy(h, c->dbg, sizeof(h), hipMemcpyDeviceToHost) == hipSuccess) {
+      const double nl = c->last_lists[2] ? (double)c->last_lists[2] : 1.0;
+      std::fprintf(stderr, "[icp dbg] iter=%d ball_list=%u ball_overflow=%llu ball_pts/query=%.1f lane_list=%u\n", iter,
+                   c->last_lists[1], h[14], c->last_lists[1] ? (double)h[15] / c->last_lists[1] : 0.0,
+                   c->last_lists[2]);
+      std::fprintf(stderr,
+                   "[icp dbg] iter=%d lane_list: visits/query=%.1f max_visits=%llu pts/query=%.1f "
+                   ">256 visits=%llu >1024 visits=%llu max_dist_mm=%llu\n",
+                   iter, (double)h[8] / nl, h[9], (double)h[10] / nl, h[11], h[12], h[13]);
       std::fprintf(stderr,
                    "[icp dbg] iter=%d waves=%llu overflow=%llu excluded=%llu coverage_fail=%llu not_cand=%llu "
                    "cand_pts/wave=%.1f leaves/wave=%.1f bfs_rounds/wave=%.2f lane_list=%u fallback=%u\n",
                    iter, h[0], h[1], h[2], h[3], h[6], h[0] ? (double)h[4] / h[0] : 0.0,
                    h[0] ? (double)h[7] / h[0] : 0.0, h[0] ? (double)h[5] / h[0] : 0.0, c->last_lists[1],
                    c->last_lists[0]);
+    }
   }
   return ICP_HIP_OK;
 }
@@ -412,16 +426,21 @@ int icp_hip_nn(icp_hip_ctx* c, const double* q, int64_t n, int32_t* idx_out, dou
     a.init_best = c->init_best;
   a.variant = c->nn_variant;
     int32_t* fbl = nullptr;
-    if (e == hipSuccess) e = dalloc(&fbl, 2 * (size_t)n);
+    double* fbu = nullptr;
+    if (e == hipSuccess) e = dalloc(&fbl, 3 * (size_t)n);
+    if (e == hipSuccess) e = dalloc(&fbu, (size_t)n);
     a.fb_list = fbl;
     a.fb_list2 = fbl + n;
+    a.fb_list3 = fbl + 2 * n;
+    a.fb_u2 = fbu;
     a.fb_count = c->fb_count;
-    if (e == hipSuccess) e = hipMemsetAsync(c->fb_count, 0, 2 * sizeof(unsigned int), c->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(c->fb_count, 0, 3 * sizeof(unsigned int), c->stream);
     if (e == hipSuccess) e = launch_nn(a, c->stream);
     if (e == hipSuccess)
-      e = hipMemcpyAsync(c->last_lists, c->fb_count, 2 * sizeof(unsigned int), hipMemcpyDeviceToHost, c->stream);
+      e = hipMemcpyAsync(c->last_lists, c->fb_count, 3 * sizeof(unsigned int), hipMemcpyDeviceToHost, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     dfree(fbl);
+    dfree(fbu);
     if (e == hipSuccess) e = launch_scatter_corr(nullptr, pos, c->pts, di, d, dd, n, c->stream);
     if (e == hipSuccess && idx_out) e = hipMemcpyAsync(idx_out, di, sizeof(int32_t) * n, hipMemcpyDeviceToHost, c->stream);
     if (e == hipSuccess && dist_out) e = hipMemcpyAsync(dist_out, dd, sizeof(double) * n, hipMemcpyDeviceToHost, c->stream);

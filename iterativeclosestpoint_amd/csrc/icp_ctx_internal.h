@@ -27,10 +27,11 @@ struct icp_hip_ctx {
   int32_t* perm = nullptr;
   int32_t* pos = nullptr;  // leaf-order position of the match
   double* dist = nullptr;  // residual
-  int32_t* fb_list = nullptr;            // queries for the exact fallback
+  int32_t* fb_list = nullptr;            // exact, ball and per-lane query lists (3 x n_src)
+  double* fb_u = nullptr;                // the ball list's distance guesses
   unsigned int* fb_count = nullptr;
   unsigned long long* dbg = nullptr;
-  unsigned int last_lists[2] = {0, 0};  // fallback / per-lane list sizes of the last search
+  unsigned int last_lists[3] = {0, 0, 0};  // exact / ball / per-lane list sizes of the last search
   icp::Moments* mparts = nullptr;
   icp::CovMoments* cparts = nullptr;
   int64_t nb_nn = 0, nb_cull = 0;

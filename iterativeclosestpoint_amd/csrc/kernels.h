@@ -41,8 +41,10 @@ struct NNLaunch {
   int count;
   int variant;  // 1 = k_nn (reference order), 2 = k_nn2, 3 = certified per-lane, 4 = wave-cooperative
   int32_t* fb_list;        // variants 3/4: queries sent to the exact fallback
-  int32_t* fb_list2;       // variant 4: queries left to the per-lane certified search
-  unsigned int* fb_count;  // [0] fallback list, [1] per-lane list; zeroed before the launch
+  int32_t* fb_list2;       // variant 4: queries a wave did not take -> one-wave ball search
+  double* fb_u2;           // variant 4: the distance guess u of each fb_list2 entry
+  int32_t* fb_list3;       // variant 4: queries left to the per-lane certified search
+  unsigned int* fb_count;  // [0] exact, [1] ball, [2] per-lane list sizes; zeroed before the launch
   hipEvent_t ev_fast_done; // optional: recorded right after the fast kernel
   int have_prev;           // variant 4: dist_out holds the previous residuals of these queries
   unsigned long long* dbg; // optional diagnostics of the wave-cooperative search (ICP_NN_DEBUG)

@@ -514,11 +514,28 @@ __device__ __forceinline__ void wave_append(bool want, int64_t i, unsigned* coun
   if (want) list[base + off] = (int32_t)i;
 }
 
+// wave_append that also stores a per-entry payload (the guess u of the ball search).
+__device__ __forceinline__ void wave_append_u(bool want, int64_t i, double u, unsigned* counter, int32_t* list,
+                                              double* payload) {
+  const unsigned long long m = __ballot(want);
+  if (m == 0) return;
+  const int lane = threadIdx.x & 63;
+  const int leader = __builtin_ctzll(m);
+  unsigned base = 0;
+  if (lane == leader) base = atomicAdd(counter, (unsigned)__popcll(m));
+  base = __shfl(base, leader, kWave);
+  const int off = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+  if (want) {
+    list[base + off] = (int32_t)i;
+    payload[base + off] = u;
+  }
+}
+
 // Per-lane certified search (the fast path of one query): nearest child first, remaining
 // siblings in octant order, level drop on the 16-bit key; tracks best, second best, position.
 __device__ __forceinline__ void fast_dfs(const NNLaunch& a, double qx, double qy, double qz,
                                          unsigned long long* st, int bs, double& best, double& second,
-                                         int32_t& bpos) {
+                                         int32_t& bpos, uint32_t& nvis, uint32_t& npts) {
   double thr = __builtin_inf();
   uint32_t thr_key = key16(__builtin_inf());
   int sp = 0;
@@ -532,8 +549,10 @@ __device__ __forceinline__ void fast_dfs(const NNLaunch& a, double qx, double qy
       const int2 topo = *reinterpret_cast<const int2*>(&a.nodes[node].first);
       const int32_t first = topo.x;
       const uint32_t meta = (uint32_t)topo.y;
+      nvis++;
       if (meta & kLeafBit) {
         const int32_t cnt = (int32_t)(meta & ~kLeafBit);
+        npts += (uint32_t)cnt;
         for (int32_t k = 0; k < cnt; k++) {
           const TgtPt* p = a.pts + first + k;
           const double2 pxy = *reinterpret_cast<const double2*>(&p->x);
@@ -636,7 +655,8 @@ __global__ void __launch_bounds__(256) k_nn3(NNLaunch a) {
 
   double best = __builtin_inf(), second = __builtin_inf();
   int32_t bpos = -1;
-  if (active && finite_q) fast_dfs(a, qx, qy, qz, lds_stack + threadIdx.x, bs, best, second, bpos);
+  uint32_t nvis = 0, npts = 0;
+  if (active && finite_q) fast_dfs(a, qx, qy, qz, lds_stack + threadIdx.x, bs, best, second, bpos, nvis, npts);
   bool ok = true;
   int32_t pos = bpos;
   double d = 0.0;
@@ -711,35 +731,77 @@ __global__ void __launch_bounds__(256) k_nn_fallback(NNLaunch a) {
   }
 }
 
-// When the fallback list is non-empty, rebuild every block's residual moments from the final
-// residuals (same blocks as k_nn3: deterministic whatever the list order).
-__global__ void __launch_bounds__(256) k_moments_fix(NNLaunch a) {
-  __shared__ double red[16];
-  if (a.fb_count[0] == 0 && a.fb_count[1] == 0) return;
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const bool active = i < a.n;
-  const double d = active ? a.dist_out[i] : 0.0;
-  double s1[2] = {active ? 1.0 : 0.0, active ? d : 0.0};
-  block_sum<2>(s1, red);
-  const double nb = s1[0];
-  const double mean = s1[1] / nb;
-  const double dev = active ? (d - mean) : 0.0;
-  const bool fin = active && __builtin_isfinite(d);
-  double s2[2] = {dev * dev, (active && !fin) ? 1.0 : 0.0};
-  block_sum<2>(s2, red);
-  double mn = fin ? d : 1.7976931348623157e308, mxv = fin ? d : 0.0;
-  block_minmax(mn, mxv, red);
-  if (threadIdx.x == 0) {
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, kWave);
+  return v;
+}
+__device__ __forceinline__ double wave_min_d(double v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    const double o = __shfl_xor(v, off, kWave);
+    v = o < v ? o : v;
+  }
+  return v;
+}
+__device__ __forceinline__ double wave_max_d(double v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    const double o = __shfl_xor(v, off, kWave);
+    v = o > v ? o : v;
+  }
+  return v;
+}
+// When a list is non-empty, rebuild every part's residual moments from the final residuals: one
+// wave per part of `a.part_size` queries (the search kernel's block), at most 4 per lane, wave
+// shuffles only. Same parts and a fixed order: deterministic whatever the list order.
+__global__ void __launch_bounds__(256) k_moments_fix(NNLaunch a, int part_size, int64_t nparts) {
+  if (a.fb_count[0] == 0 && a.fb_count[1] == 0 && a.fb_count[2] == 0) return;
+  const int lane = threadIdx.x & 63;
+  const int64_t part = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (part >= nparts) return;
+  const int64_t b0 = part * part_size;
+  double d[4];
+  int cnt = 0;
+  double s = 0.0;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const int e = lane + 64 * k;
+    const int64_t i = b0 + e;
+    const bool act = e < part_size && i < a.n;
+    d[k] = act ? a.dist_out[i] : 0.0;
+    cnt += act ? 1 : 0;
+    s += act ? d[k] : 0.0;
+  }
+  const double nb = wave_sum_d((double)cnt);
+  const double mean = wave_sum_d(s) / nb;
+  double m2 = 0.0, bad = 0.0, mn = 1.7976931348623157e308, mx = 0.0;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const int e = lane + 64 * k;
+    const bool act = e < part_size && b0 + e < a.n;
+    const double dev = act ? d[k] - mean : 0.0;
+    m2 += dev * dev;
+    const bool fin = act && __builtin_isfinite(d[k]);
+    bad += (act && !fin) ? 1.0 : 0.0;
+    mn = fin && d[k] < mn ? d[k] : mn;
+    mx = fin && d[k] > mx ? d[k] : mx;
+  }
+  m2 = wave_sum_d(m2);
+  bad = wave_sum_d(bad);
+  mn = wave_min_d(mn);
+  mx = wave_max_d(mx);
+  if (lane == 0) {
     Moments m;
     m.n = nb;
     m.mean = mean;
-    m.m2 = s2[0];
+    m.m2 = m2;
     m.dmin = mn;
-    m.dmax = mxv;
-    m.nbad = s2[1];
+    m.dmax = mx;
+    m.nbad = bad;
     m.pad0 = 0.0;
     m.pad1 = 0.0;
-    a.part[blockIdx.x] = m;
+    a.part[part] = m;
   }
 }
 
@@ -763,27 +825,6 @@ constexpr int kWaveLdsBytes = 2 * kWaveFrontier * 4 + kWavePoints * 4 + 64 * 32;
 
 __device__ __forceinline__ void wave_lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
-__device__ __forceinline__ double wave_sum_d(double v) {
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, kWave);
-  return v;
-}
-__device__ __forceinline__ double wave_min_d(double v) {
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) {
-    const double o = __shfl_xor(v, off, kWave);
-    v = o < v ? o : v;
-  }
-  return v;
-}
-__device__ __forceinline__ double wave_max_d(double v) {
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) {
-    const double o = __shfl_xor(v, off, kWave);
-    v = o > v ? o : v;
-  }
-  return v;
-}
 __device__ __forceinline__ int wave_incl_scan(int v, int lane) {
 #pragma unroll
   for (int off = 1; off < 64; off <<= 1) {
@@ -1052,7 +1093,8 @@ __global__ void __launch_bounds__(256) k_nn4(NNLaunch a) {
     }
   }
   wave_append(to_exact, i, a.fb_count, a.fb_list);
-  wave_append(to_lane, i, a.fb_count + 1, a.fb_list2);
+  const bool covered = !(join && !(best <= u));
+  wave_append_u(to_lane, i, covered ? u : __builtin_inf(), a.fb_count + 1, a.fb_list2, a.fb_u2);
   if (!a.part) return;
   __syncthreads();
   double* red = reinterpret_cast<double*>(lds_stack);
@@ -1081,21 +1123,182 @@ __global__ void __launch_bounds__(256) k_nn4(NNLaunch a) {
   }
 }
 
-// Per-lane certified search over the queries a wave did not take (compacted: full waves).
+// One wave per query for the queries a k_nn4 wave did not take (outliers far from the surface,
+// waves whose candidate set overflowed). The guess u bounds the query's nearest distance: the
+// wave collects, breadth-first, every leaf whose box distance s <= u (1 + 2^-47) — a sphere test,
+// tighter than k_nn4's box — and scans their points one per lane. Certification as in k_nn4
+// (best <= u and the window test). Leaves of boxes with s > u (1 + 2^-47) only hold points with
+// fl(d2) > best (1 + 2^-48) (monotone rounding, see k_nn3), so nothing in the window is missed.
+// No usable guess or an overflowing candidate set -> per-lane search (k_nn3_list).
+constexpr int kBallFrontier = 256;
+constexpr int kBallPoints = 1024;
+constexpr int kBallLdsBytes = 2 * kBallFrontier * 4 + kBallPoints * 4;
+
+__global__ void __launch_bounds__(64) k_nn_ball(NNLaunch a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned long long lds_stack[];
+  int32_t* fr0 = reinterpret_cast<int32_t*>(lds_stack);
+  int32_t* fr1 = fr0 + kBallFrontier;
+  int32_t* plist = fr1 + kBallFrontier;
+  const int lane = threadIdx.x;
+  const unsigned cnt = a.fb_count[1];
+  for (unsigned j = blockIdx.x; j < cnt; j += gridDim.x) {
+    const int64_t i = a.fb_list2[j];
+    const double u = a.fb_u2[j];
+    const double qx = a.x[i], qy = a.y[i], qz = a.z[i];
+    if (!(u <= 0x1p900)) {
+      if (lane == 0) a.fb_list3[atomicAdd(a.fb_count + 2, 1u)] = (int32_t)i;
+      continue;
+    }
+    const double thr = u * (1.0 + kFastPrune);
+    int nf = 1, npts = 0;
+    bool overflow = false;
+    int32_t* cur = fr0;
+    int32_t* nxt = fr1;
+    wave_lds_fence();
+    if (lane == 0) cur[0] = 0;
+    wave_lds_fence();
+    while (nf > 0) {
+      int nn = 0;
+      for (int base = 0; base < nf; base += 64) {
+        const int jj = base + lane;
+        const bool has = jj < nf;
+        bool leaf = false;
+        int32_t first = 0;
+        uint32_t meta = 0, kids = 0;
+        if (has) {
+          const NodeRec* rr = a.nodes + cur[jj];
+          const int2 topo = *reinterpret_cast<const int2*>(&rr->first);
+          first = topo.x;
+          meta = (uint32_t)topo.y;
+          leaf = (meta & kLeafBit) != 0;
+          if (!leaf) {
+            const double2 l01 = *reinterpret_cast<const double2*>(&rr->lo[0]);
+            const double2 l2h0 = *reinterpret_cast<const double2*>(&rr->lo[2]);
+            const double2 h12 = *reinterpret_cast<const double2*>(&rr->hi[1]);
+            const double lx = l01.x, ly = l01.y, lz = l2h0.x, hx = l2h0.y, hy = h12.x, hz = h12.y;
+            const double mx = (lx + hx) / 2, my = (ly + hy) / 2, mz = (lz + hz) / 2;
+            const double ax0 = smax(0.0, smax(lx - qx, qx - mx)), ax1 = smax(0.0, smax(mx - qx, qx - hx));
+            const double ay0 = smax(0.0, smax(ly - qy, qy - my)), ay1 = smax(0.0, smax(my - qy, qy - hy));
+            const double az0 = smax(0.0, smax(lz - qz, qz - mz)), az1 = smax(0.0, smax(mz - qz, qz - hz));
+            const double sx[2] = {ax0 * ax0, ax1 * ax1};
+            const double sy[2] = {ay0 * ay0, ay1 * ay1};
+            const double sz[2] = {az0 * az0, az1 * az1};
+            const uint32_t mask = meta & 0xffu;
+#pragma unroll
+            for (int o = 0; o < 8; o++) {
+              const double c = sx[o & 1] + sy[(o >> 1) & 1] + sz[o >> 2];
+              kids |= (((mask >> o) & 1u) && !(c > thr)) ? (1u << o) : 0u;
+            }
+          }
+        }
+        const int lcnt = (has && leaf) ? (int)(meta & ~kLeafBit) : 0;
+        const int lincl = wave_incl_scan(lcnt, lane);
+        const int ltot = __shfl(lincl, 63, kWave);
+        const int lpos = npts + lincl - lcnt;
+        if (lcnt > 0 && lpos + lcnt <= kBallPoints)
+          for (int c = 0; c < lcnt; c++) plist[lpos + c] = first + c;
+        npts += ltot;
+        const int nch = __builtin_popcount(kids);
+        const int incl = wave_incl_scan(nch, lane);
+        const int tot = __shfl(incl, 63, kWave);
+        int off = nn + incl - nch;
+        if (off + nch <= kBallFrontier) {
+          const uint32_t mask = meta & 0xffu;
+          uint32_t kk = kids;
+          while (kk) {
+            const uint32_t o = (uint32_t)__builtin_ctz(kk);
+            kk &= kk - 1u;
+            nxt[off++] = first + __builtin_popcount(mask & ((1u << o) - 1u));
+          }
+        }
+        nn += tot;
+      }
+      if (npts > kBallPoints || nn > kBallFrontier) {
+        overflow = true;
+        break;
+      }
+      int32_t* t = cur;
+      cur = nxt;
+      nxt = t;
+      nf = nn;
+      wave_lds_fence();
+    }
+    if (a.dbg && lane == 0) {
+      atomicAdd(&a.dbg[14], overflow ? 1ull : 0ull);
+      atomicAdd(&a.dbg[15], (unsigned long long)npts);
+    }
+    if (overflow) {
+      if (lane == 0) a.fb_list3[atomicAdd(a.fb_count + 2, 1u)] = (int32_t)i;
+      wave_lds_fence();
+      continue;
+    }
+    wave_lds_fence();
+    double best = __builtin_inf(), second = __builtin_inf();
+    int32_t bpos = 0x7fffffff;
+    for (int k = lane; k < npts; k += 64) {
+      const int32_t g = plist[k];
+      const TgtPt* p = a.pts + g;
+      const double2 xy = *reinterpret_cast<const double2*>(&p->x);
+      const double dx = xy.x - qx, dy = xy.y - qy, dz = p->z - qz;
+      const double d2 = dx * dx + dy * dy + dz * dz;
+      if (d2 < best) {
+        second = best;
+        best = d2;
+        bpos = g;
+      } else if (d2 < second) {
+        second = d2;
+      }
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      const double ob = __shfl_xor(best, o, kWave);
+      const double os = __shfl_xor(second, o, kWave);
+      const int32_t op = __shfl_xor(bpos, o, kWave);
+      const double lo_ = ob < best ? ob : best;
+      const double hi_ = ob < best ? best : ob;
+      const double ss = os < second ? os : second;
+      second = hi_ < ss ? hi_ : ss;
+      bpos = (ob < best || (ob == best && op < bpos)) ? op : bpos;
+      best = lo_;
+    }
+    if (lane == 0) {
+      if (!(best <= u)) {
+        a.fb_list3[atomicAdd(a.fb_count + 2, 1u)] = (int32_t)i;
+      } else if (certified(best, second, a.init_best)) {
+        a.pos_out[i] = bpos;
+        a.dist_out[i] = __builtin_sqrt(best);
+      } else {
+        a.fb_list[atomicAdd(a.fb_count, 1u)] = (int32_t)i;
+      }
+    }
+    wave_lds_fence();
+  }
+}
+
+// Per-lane certified search over the queries the ball search left (compacted: full waves).
 __global__ void __launch_bounds__(256) k_nn3_list(NNLaunch a) {
   extern __shared__ __attribute__((aligned(16))) unsigned long long lds_stack[];
-  const unsigned cnt = a.fb_count[1];
+  const unsigned cnt = a.fb_count[2];
   for (unsigned j0 = blockIdx.x * blockDim.x; j0 < cnt; j0 += gridDim.x * blockDim.x) {
     const unsigned j = j0 + threadIdx.x;
     const bool act = j < cnt;
-    const int64_t i = act ? a.fb_list2[j] : 0;
+    const int64_t i = act ? a.fb_list3[j] : 0;
     bool ok = false;
     if (act) {
       const double qx = a.x[i], qy = a.y[i], qz = a.z[i];
       double best = __builtin_inf(), second = __builtin_inf();
       int32_t bpos = -1;
-      fast_dfs(a, qx, qy, qz, lds_stack + threadIdx.x, blockDim.x, best, second, bpos);
+      uint32_t nvis = 0, npts = 0;
+      fast_dfs(a, qx, qy, qz, lds_stack + threadIdx.x, blockDim.x, best, second, bpos, nvis, npts);
       ok = certified(best, second, a.init_best);
+      if (a.dbg) {
+        atomicAdd(&a.dbg[8], (unsigned long long)nvis);
+        atomicMax(&a.dbg[9], (unsigned long long)nvis);
+        atomicAdd(&a.dbg[10], (unsigned long long)npts);
+        if (nvis > 256) atomicAdd(&a.dbg[11], 1ull);
+        if (nvis > 1024) atomicAdd(&a.dbg[12], 1ull);
+        atomicMax(&a.dbg[13], (unsigned long long)__builtin_sqrt(best) * 1000ull);
+      }
       if (ok) {
         a.pos_out[i] = bpos;
         a.dist_out[i] = __builtin_sqrt(best);
@@ -1352,9 +1555,12 @@ hipError_t launch_nn(const NNLaunch& a, hipStream_t s) {
     const unsigned lgrid = (unsigned)((a.n + 63) / 64 < 4096 ? (a.n + 63) / 64 : 4096);
     const size_t lshm = (size_t)levels * 64 * sizeof(unsigned long long) < 1024 ? 1024
                         : (size_t)levels * 64 * sizeof(unsigned long long);
+    const unsigned bgrid = (unsigned)((a.n < 16384) ? a.n : 16384);
+    hipLaunchKernelGGL(k_nn_ball, dim3(bgrid), dim3(64), kBallLdsBytes, s, a);
     hipLaunchKernelGGL(k_nn3_list, dim3(lgrid), dim3(64), lshm, s, a);
     hipLaunchKernelGGL(k_nn_fallback, dim3(lgrid), dim3(64), lshm, s, a);
-    if (a.part) hipLaunchKernelGGL(k_moments_fix, dim3(grid), dim3(bs), 0, s, a);
+    if (a.part) hipLaunchKernelGGL(k_moments_fix, dim3((unsigned)((grid + 3) / 4)), dim3(256), 0, s, a, bs,
+                                   (int64_t)grid);
     return hipGetLastError();
   }
   if (a.variant == 3 && !a.count) {
@@ -1364,7 +1570,8 @@ hipError_t launch_nn(const NNLaunch& a, hipStream_t s) {
     if (a.ev_fast_done) (void)hipEventRecord(a.ev_fast_done, s);
     const unsigned fb_grid = grid < 1024u ? grid : 1024u;
     hipLaunchKernelGGL(k_nn_fallback, dim3(fb_grid), dim3(bs), shmem, s, a);
-    if (a.part) hipLaunchKernelGGL(k_moments_fix, dim3(grid), dim3(bs), 0, s, a);
+    if (a.part) hipLaunchKernelGGL(k_moments_fix, dim3((unsigned)((grid + 3) / 4)), dim3(256), 0, s, a, bs,
+                                   (int64_t)grid);
     return hipGetLastError();
   }
   if (a.variant == 1 || a.count) {
