@@ -105,6 +105,8 @@ int icp_hip_create(icp_hip_ctx** out, int device) {
   icp_hip_ctx* c = new icp_hip_ctx();
   c->device = device;
   if (const char* v = std::getenv("ICP_NN_VARIANT")) c->nn_variant = std::atoi(v);
+  if (const char* v = std::getenv("ICP_SCAN_GROUP")) c->scan_group = std::atoi(v);
+  if (const char* v = std::getenv("ICP_WAVE_POINTS")) c->wave_points = std::atoi(v);
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
     delete c;
     return fail(ICP_HIP_EDEVICE, "hipStreamCreate failed");
@@ -218,7 +220,7 @@ int icp_hip_set_source(icp_hip_ctx* c, const double* xyz, int64_t n) {
   if (n == 0) return ICP_HIP_OK;
   // Spatially compact query order (kd buckets of 64 = one wave), computed on the host.
   std::vector<int32_t> perm;
-  kd_query_order(xyz, n, 64, &perm);
+  kd_query_order(xyz, n, 8, &perm);
   std::vector<double> reordered((size_t)(3 * n));
   for (int64_t k = 0; k < n; k++) {
     const double* p = xyz + 3 * (int64_t)perm[k];
@@ -265,6 +267,8 @@ int icp_hip_iterate(icp_hip_ctx* c, const double* T_apply, int iter, int rules, 
   a.levels = c->levels;
   a.init_best = c->init_best;
   a.variant = c->nn_variant;
+  a.scan_group = c->scan_group;
+  a.wave_points = c->wave_points;
   a.apply = T_apply ? 1 : 0;
   if (T_apply)
     for (int k = 0; k < 12; k++) a.T[k] = T_apply[k];
@@ -276,8 +280,8 @@ int icp_hip_iterate(icp_hip_ctx* c, const double* T_apply, int iter, int rules, 
   a.have_prev = c->have_prev ? 1 : 0;
   HIP_TRY(hipMemsetAsync(c->fb_count, 0, 3 * sizeof(unsigned int), s));
   if (std::getenv("ICP_NN_DEBUG")) {
-    if (!c->dbg) HIP_TRY(dalloc(&c->dbg, 16));
-    HIP_TRY(hipMemsetAsync(c->dbg, 0, 16 * sizeof(unsigned long long), s));
+    if (!c->dbg) HIP_TRY(dalloc(&c->dbg, 24));
+    HIP_TRY(hipMemsetAsync(c->dbg, 0, 24 * sizeof(unsigned long long), s));
     a.dbg = c->dbg;
   }
   HIP_TRY(hipEventRecord(c->ev_nn0, s));
@@ -331,8 +335,11 @@ int icp_hip_iterate(icp_hip_ctx* c, const double* T_apply, int iter, int rules, 
   c->have_results = true;
   c->have_prev = true;
   if (c->dbg && std::getenv("ICP_NN_DEBUG")) {
-    unsigned long long h[16];
+    unsigned long long h[24];
     if (hipMemcpy(h, c->dbg, sizeof(h), hipMemcpyDeviceToHost) == hipSuccess) {
+      const double w = h[0] ? (double)h[0] : 1.0;
+      std::fprintf(stderr, "[icp dbg] iter=%d wave clocks: guess+box=%.0f walk=%.0f scan=%.0f finish=%.0f\n", iter,
+                   (double)h[16] / w, (double)h[17] / w, (double)h[18] / w, (double)h[19] / w);
       const double nl = c->last_lists[2] ? (double)c->last_lists[2] : 1.0;
       std::fprintf(stderr, "[icp dbg] iter=%d ball_list=%u ball_overflow=%llu ball_pts/query=%.1f lane_list=%u\n", iter,
                    c->last_lists[1], h[14], c->last_lists[1] ? (double)h[15] / c->last_lists[1] : 0.0,
@@ -425,6 +432,8 @@ int icp_hip_nn(icp_hip_ctx* c, const double* q, int64_t n, int32_t* idx_out, dou
     a.levels = c->levels;
     a.init_best = c->init_best;
   a.variant = c->nn_variant;
+  a.scan_group = c->scan_group;
+  a.wave_points = c->wave_points;
     int32_t* fbl = nullptr;
     double* fbu = nullptr;
     if (e == hipSuccess) e = dalloc(&fbl, 3 * (size_t)n);
@@ -473,6 +482,8 @@ int icp_hip_traversal_counts(icp_hip_ctx* c, double* mean_entries, double* mean_
   a.levels = c->levels;
   a.init_best = c->init_best;
   a.variant = c->nn_variant;
+  a.scan_group = c->scan_group;
+  a.wave_points = c->wave_points;
   a.count = 1;
   HIP_TRY(launch_nn(a, c->stream));
   unsigned long long h[2] = {0, 0};

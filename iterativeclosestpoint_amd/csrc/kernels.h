@@ -47,6 +47,8 @@ struct NNLaunch {
   unsigned int* fb_count;  // [0] exact, [1] ball, [2] per-lane list sizes; zeroed before the launch
   hipEvent_t ev_fast_done; // optional: recorded right after the fast kernel
   int have_prev;           // variant 4: dist_out holds the previous residuals of these queries
+  int scan_group;          // variant 4: lanes per scan group (8, 16, 32 or 64 = whole wave)
+  int wave_points;         // variant 4: candidate-list capacity per wave (512, 768 or 1024)
   unsigned long long* dbg; // optional diagnostics of the wave-cooperative search (ICP_NN_DEBUG)
 };
 

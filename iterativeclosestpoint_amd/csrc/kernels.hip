@@ -32,13 +32,67 @@ __device__ __forceinline__ double box_dist(double lx, double ly, double lz, doub
   return __builtin_sqrt(dx * dx + dy * dy + dz * dz);
 }
 
+// Wave-wide reductions and scans on DPP (row shifts within 16-lane rows, then row_bcast15/31
+// across rows), no LDS traffic. Must be called with every lane of the wave active.
+template <int CTRL, int RM, bool ZERO>
+__device__ __forceinline__ double dpp_d(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = (int)(unsigned)b, hi = (int)(b >> 32);
+  const int rlo = __builtin_amdgcn_update_dpp(ZERO ? 0 : lo, lo, CTRL, RM, 0xf, ZERO);
+  const int rhi = __builtin_amdgcn_update_dpp(ZERO ? 0 : hi, hi, CTRL, RM, 0xf, ZERO);
+  return __longlong_as_double((long long)(((unsigned long long)(unsigned)rhi << 32) | (unsigned)rlo));
+}
+__device__ __forceinline__ double lane63_d(double v) {
+  const long long b = __double_as_longlong(v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)b, 63);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(b >> 32), 63);
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+__device__ __forceinline__ double wave_sum_d(double v) {
+  v += dpp_d<0x111, 0xf, true>(v);
+  v += dpp_d<0x112, 0xf, true>(v);
+  v += dpp_d<0x114, 0xf, true>(v);
+  v += dpp_d<0x118, 0xf, true>(v);
+  v += dpp_d<0x142, 0xa, true>(v);
+  v += dpp_d<0x143, 0xc, true>(v);
+  return lane63_d(v);
+}
+__device__ __forceinline__ double dmin_(double a, double b) { return b < a ? b : a; }
+__device__ __forceinline__ double dmax_(double a, double b) { return b > a ? b : a; }
+__device__ __forceinline__ double wave_min_d(double v) {
+  v = dmin_(v, dpp_d<0x111, 0xf, false>(v));
+  v = dmin_(v, dpp_d<0x112, 0xf, false>(v));
+  v = dmin_(v, dpp_d<0x114, 0xf, false>(v));
+  v = dmin_(v, dpp_d<0x118, 0xf, false>(v));
+  v = dmin_(v, dpp_d<0x142, 0xa, false>(v));
+  v = dmin_(v, dpp_d<0x143, 0xc, false>(v));
+  return lane63_d(v);
+}
+__device__ __forceinline__ double wave_max_d(double v) {
+  v = dmax_(v, dpp_d<0x111, 0xf, false>(v));
+  v = dmax_(v, dpp_d<0x112, 0xf, false>(v));
+  v = dmax_(v, dpp_d<0x114, 0xf, false>(v));
+  v = dmax_(v, dpp_d<0x118, 0xf, false>(v));
+  v = dmax_(v, dpp_d<0x142, 0xa, false>(v));
+  v = dmax_(v, dpp_d<0x143, 0xc, false>(v));
+  return lane63_d(v);
+}
+// Inclusive prefix sum over the wave's lanes; *total = the wave's sum (uniform).
+__device__ __forceinline__ int wave_incl_scan(int v, int* total) {
+  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, true);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, true);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, true);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, true);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);
+  *total = __builtin_amdgcn_readlane(v, 63);
+  return v;
+}
+
 template <int N>
 __device__ __forceinline__ void block_sum(double (&v)[N], double* red) {
 #pragma unroll
-  for (int off = kWave / 2; off >= 1; off >>= 1) {
-#pragma unroll
-    for (int k = 0; k < N; k++) v[k] += __shfl_xor(v[k], off, kWave);
-  }
+  for (int k = 0; k < N; k++) v[k] = wave_sum_d(v[k]);
   const int w = threadIdx.x / kWave, lane = threadIdx.x % kWave, nw = blockDim.x / kWave;
   if (lane == 0) {
 #pragma unroll
@@ -55,13 +109,8 @@ __device__ __forceinline__ void block_sum(double (&v)[N], double* red) {
 }
 
 __device__ __forceinline__ void block_minmax(double& mn, double& mx, double* red) {
-#pragma unroll
-  for (int off = kWave / 2; off >= 1; off >>= 1) {
-    const double a = __shfl_xor(mn, off, kWave);
-    const double b = __shfl_xor(mx, off, kWave);
-    mn = a < mn ? a : mn;
-    mx = b > mx ? b : mx;
-  }
+  mn = wave_min_d(mn);
+  mx = wave_max_d(mx);
   const int w = threadIdx.x / kWave, lane = threadIdx.x % kWave, nw = blockDim.x / kWave;
   if (lane == 0) {
     red[2 * w] = mn;
@@ -509,7 +558,7 @@ __device__ __forceinline__ void wave_append(bool want, int64_t i, unsigned* coun
   const int leader = __builtin_ctzll(m);
   unsigned base = 0;
   if (lane == leader) base = atomicAdd(counter, (unsigned)__popcll(m));
-  base = __shfl(base, leader, kWave);
+  base = (unsigned)__builtin_amdgcn_readlane((int)base, leader);
   const int off = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
   if (want) list[base + off] = (int32_t)i;
 }
@@ -523,7 +572,7 @@ __device__ __forceinline__ void wave_append_u(bool want, int64_t i, double u, un
   const int leader = __builtin_ctzll(m);
   unsigned base = 0;
   if (lane == leader) base = atomicAdd(counter, (unsigned)__popcll(m));
-  base = __shfl(base, leader, kWave);
+  base = (unsigned)__builtin_amdgcn_readlane((int)base, leader);
   const int off = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
   if (want) {
     list[base + off] = (int32_t)i;
@@ -731,27 +780,6 @@ __global__ void __launch_bounds__(256) k_nn_fallback(NNLaunch a) {
   }
 }
 
-__device__ __forceinline__ double wave_sum_d(double v) {
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, kWave);
-  return v;
-}
-__device__ __forceinline__ double wave_min_d(double v) {
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) {
-    const double o = __shfl_xor(v, off, kWave);
-    v = o < v ? o : v;
-  }
-  return v;
-}
-__device__ __forceinline__ double wave_max_d(double v) {
-#pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) {
-    const double o = __shfl_xor(v, off, kWave);
-    v = o > v ? o : v;
-  }
-  return v;
-}
 // When a list is non-empty, rebuild every part's residual moments from the final residuals: one
 // wave per part of `a.part_size` queries (the search kernel's block), at most 4 per lane, wave
 // shuffles only. Same parts and a fixed order: deterministic whatever the list order.
@@ -820,31 +848,36 @@ __global__ void __launch_bounds__(256) k_moments_fix(NNLaunch a, int part_size, 
 // for the per-lane certified search (k_nn3_list); uncertified ones for the exact DFS.
 
 constexpr int kWaveFrontier = 256;  // node ids per frontier buffer (two buffers)
-constexpr int kWavePoints = 1024;   // candidate point positions per wave
-constexpr int kWaveLdsBytes = 2 * kWaveFrontier * 4 + kWavePoints * 4 + 64 * 32;  // + staging
+constexpr int kMaxGroups = 8;       // lane groups of the scan (GL = 8 lanes at the finest)
+// per wave: two frontier buffers (reused as the 64-point staging area once the walk is done),
+// the candidate list, the group boxes and the group index lists
+__host__ __device__ constexpr int wave_lds_bytes(int gl, int pl) {
+  return 2 * kWaveFrontier * 4 + pl * 4 + (gl < 64 ? kMaxGroups * 64 * 2 : 0);
+}
+static_assert(2 * kWaveFrontier * 4 >= 64 * 32, "staging area aliases the frontier buffers");
 
 __device__ __forceinline__ void wave_lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
-__device__ __forceinline__ int wave_incl_scan(int v, int lane) {
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const int t = __shfl_up(v, off, kWave);
-    if (lane >= off) v += t;
-  }
-  return v;
-}
 
-template <bool APPLY>
+// GL = lanes per scan group. GL = 64: the wave scans every staged point of its box B. GL < 64:
+// the wave's lanes form 64/GL aligned kd sub-buckets (query order), each with its own box
+// B_g (union of its joined lanes' balls, inside B); a lane scans only the staged points of its
+// group's box, the groups in parallel, so the lockstep loop runs max_g |B_g ∩ chunk| times.
+template <bool APPLY, int GL, int PL>
 __global__ void __launch_bounds__(256) k_nn4(NNLaunch a) {
+  static_assert(GL == 64 || (GL >= 8 && 64 % GL == 0), "lane group size");
+  constexpr int G = 64 / GL;
   extern __shared__ __attribute__((aligned(16))) unsigned long long lds_stack[];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const bool active = i < a.n;
-  unsigned char* wl = reinterpret_cast<unsigned char*>(lds_stack) + wv * kWaveLdsBytes;
+  unsigned char* wl = reinterpret_cast<unsigned char*>(lds_stack) + wv * wave_lds_bytes(GL, PL);
   int32_t* fr0 = reinterpret_cast<int32_t*>(wl);
   int32_t* fr1 = fr0 + kWaveFrontier;
-  int32_t* plist = fr1 + kWaveFrontier;                               // candidate points
-  double4* stage = reinterpret_cast<double4*>(plist + kWavePoints);   // 64 staged points
+  double4* stage = reinterpret_cast<double4*>(wl);                  // after the walk only
+  int32_t* plist = fr1 + kWaveFrontier;                             // candidate points
+  double* gbox = reinterpret_cast<double*>(plist + PL);    // G x 8 doubles
+  unsigned char* gidx = reinterpret_cast<unsigned char*>(gbox + 8 * kMaxGroups);  // G x 64
 
   double qx = 0.0, qy = 0.0, qz = 0.0, ox = 0.0, oy = 0.0, oz = 0.0;
   if (active) {
@@ -855,6 +888,7 @@ __global__ void __launch_bounds__(256) k_nn4(NNLaunch a) {
   nn_load_query<APPLY>(a, i, active, qx, qy, qz);
   const bool finite_q = __builtin_isfinite(qx) && __builtin_isfinite(qy) && __builtin_isfinite(qz);
 
+  const unsigned long long t_p0 = a.dbg ? __builtin_amdgcn_s_memtime() : 0ull;
   // Phase 1: a guess u of the nearest squared distance. After an iteration on the same queries:
   // (previous residual + displacement of the query)^2, by the triangle inequality (any guess is
   // safe: certification below also requires best <= u). Otherwise descend (nearest child, no
@@ -919,7 +953,41 @@ __global__ void __launch_bounds__(256) k_nn4(NNLaunch a) {
   const double bhx = wave_max_d(join ? qx + r : -__builtin_inf());
   const double bhy = wave_max_d(join ? qy + r : -__builtin_inf());
   const double bhz = wave_max_d(join ? qz + r : -__builtin_inf());
+  if constexpr (GL < 64) {
+    auto gmin = [](double v) {
+#pragma unroll
+      for (int off = GL / 2; off >= 1; off >>= 1) {
+        const double o = __shfl_xor(v, off, kWave);
+        v = o < v ? o : v;
+      }
+      return v;
+    };
+    auto gmax = [](double v) {
+#pragma unroll
+      for (int off = GL / 2; off >= 1; off >>= 1) {
+        const double o = __shfl_xor(v, off, kWave);
+        v = o > v ? o : v;
+      }
+      return v;
+    };
+    const double g0 = gmin(join ? qx - r : __builtin_inf());
+    const double g1 = gmin(join ? qy - r : __builtin_inf());
+    const double g2 = gmin(join ? qz - r : __builtin_inf());
+    const double g3 = gmax(join ? qx + r : -__builtin_inf());
+    const double g4 = gmax(join ? qy + r : -__builtin_inf());
+    const double g5 = gmax(join ? qz + r : -__builtin_inf());
+    if ((lane & (GL - 1)) == 0) {
+      double* gb = gbox + 8 * (lane / GL);
+      gb[0] = g0;
+      gb[1] = g1;
+      gb[2] = g2;
+      gb[3] = g3;
+      gb[4] = g4;
+      gb[5] = g5;
+    }
+  }
 
+  const unsigned long long t_p2 = a.dbg ? __builtin_amdgcn_s_memtime() : 0ull;
   // Phase 3: cooperative breadth-first collection of the leaves meeting B.
   int nleaf = 0;
   bool overflow = false;
@@ -965,15 +1033,15 @@ __global__ void __launch_bounds__(256) k_nn4(NNLaunch a) {
         }
         // a leaf contributes its points (contiguous in leaf order) to the candidate list
         const int lcnt = (has && leaf) ? (int)(meta & ~kLeafBit) : 0;
-        const int lincl = wave_incl_scan(lcnt, lane);
-        const int ltot = __shfl(lincl, 63, kWave);
+        int ltot;
+        const int lincl = wave_incl_scan(lcnt, &ltot);
         const int lpos = nleaf + lincl - lcnt;
-        if (lcnt > 0 && lpos + lcnt <= kWavePoints)
+        if (lcnt > 0 && lpos + lcnt <= PL)
           for (int c = 0; c < lcnt; c++) plist[lpos + c] = first + c;
         nleaf += ltot;
         const int nch = __builtin_popcount(kids);
-        const int incl = wave_incl_scan(nch, lane);
-        const int tot = __shfl(incl, 63, kWave);
+        int tot;
+        const int incl = wave_incl_scan(nch, &tot);
         int off = nn + incl - nch;
         if (off + nch <= kWaveFrontier) {
           const uint32_t mask = meta & 0xffu;
@@ -986,7 +1054,7 @@ __global__ void __launch_bounds__(256) k_nn4(NNLaunch a) {
         }
         nn += tot;
       }
-      if (nleaf > kWavePoints || nn > kWaveFrontier) {
+      if (nleaf > PL || nn > kWaveFrontier) {
         overflow = true;
         break;
       }
@@ -1004,6 +1072,7 @@ __global__ void __launch_bounds__(256) k_nn4(NNLaunch a) {
     if (overflow) atomicAdd(&a.dbg[1], 1ull);
   }
 
+  const unsigned long long t_p3 = a.dbg ? __builtin_amdgcn_s_memtime() : 0ull;
   // Phase 4: every joined lane scans the candidate points in lockstep: 64 points per chunk are
   // gathered by one load per lane (the next chunk's gather is in flight while the current one is
   // scanned from LDS by broadcast reads).
@@ -1011,7 +1080,7 @@ __global__ void __launch_bounds__(256) k_nn4(NNLaunch a) {
   int32_t bpos = -1;
   const int npts = nleaf;
   int scanned_pts = 0;
-  if (__ballot(join) != 0 && npts > 0) {
+  if (GL == 64 && __ballot(join) != 0 && npts > 0) {
     // Points outside B are farther than r from every joined lane (each ball lies in B), so
     // they can neither be a joined lane's nearest point nor sit in its certificate window.
     wave_lds_fence();
@@ -1055,6 +1124,61 @@ __global__ void __launch_bounds__(256) k_nn4(NNLaunch a) {
     }
     if (a.dbg && lane == 0) atomicAdd(&a.dbg[4], (unsigned long long)scanned_pts);
   }
+  if (GL < 64 && __ballot(join) != 0 && npts > 0) {
+    // Each joined lane's ball lies in its group's box B_g (inside B), so the points of B_g
+    // hold every point the lane's certificate needs. Lane l stages chunk point l (unfiltered),
+    // tests it against every B_g and appends its slot to the group lists; then each lane walks
+    // its own group's list, branch-free.
+    const int mg = lane / GL;
+    wave_lds_fence();
+    double4 nxtp = make_double4(0.0, 0.0, 0.0, 0.0);
+    if (lane < npts) {
+      const int32_t g = plist[lane];
+      const TgtPt* p = a.pts + g;
+      const double2 xy = *reinterpret_cast<const double2*>(&p->x);
+      nxtp = make_double4(xy.x, xy.y, p->z, __longlong_as_double((long long)g));
+    }
+    for (int base = 0; base < npts; base += 64) {
+      const bool have = base + lane < npts;
+      wave_lds_fence();  // the previous chunk's reads are done before the slots are rewritten
+      stage[lane] = nxtp;
+      int mycnt = 0, maxcnt = 0;
+#pragma unroll
+      for (int g = 0; g < G; g++) {
+        const double* gb = gbox + 8 * g;
+        const bool in = have && nxtp.x >= gb[0] && nxtp.x <= gb[3] && nxtp.y >= gb[1] && nxtp.y <= gb[4] &&
+                        nxtp.z >= gb[2] && nxtp.z <= gb[5];
+        const unsigned long long m = __ballot(in);
+        const int slot = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+        if (in) gidx[64 * g + slot] = (unsigned char)lane;
+        const int c = __popcll(m);
+        mycnt = (g == mg) ? c : mycnt;
+        maxcnt = c > maxcnt ? c : maxcnt;
+      }
+      wave_lds_fence();
+      const int nb = base + 64;
+      if (nb + lane < npts) {
+        const int32_t g = plist[nb + lane];
+        const TgtPt* p = a.pts + g;
+        const double2 xy = *reinterpret_cast<const double2*>(&p->x);
+        nxtp = make_double4(xy.x, xy.y, p->z, __longlong_as_double((long long)g));
+      }
+      scanned_pts += maxcnt;
+      const unsigned char* my = gidx + 64 * mg;
+      for (int k = 0; k < maxcnt; k++) {
+        const bool valid = k < mycnt;
+        const double4 pt = stage[my[k] & 63];
+        const double dx = pt.x - qx, dy = pt.y - qy, dz = pt.z - qz;
+        const double d2 = dx * dx + dy * dy + dz * dz;
+        const bool lt = valid && d2 < best;
+        const bool ls = valid && d2 < second;
+        second = lt ? best : (ls ? d2 : second);
+        best = lt ? d2 : best;
+        bpos = lt ? (int32_t)__double_as_longlong(pt.w) : bpos;
+      }
+    }
+    if (a.dbg && lane == 0) atomicAdd(&a.dbg[4], (unsigned long long)scanned_pts);
+  }
   if (a.dbg) {
     const unsigned long long ex = __ballot(cand && !join && !overflow);
     const unsigned long long cov = __ballot(join && !(best <= u));
@@ -1067,6 +1191,7 @@ __global__ void __launch_bounds__(256) k_nn4(NNLaunch a) {
     }
   }
 
+  const unsigned long long t_p4 = a.dbg ? __builtin_amdgcn_s_memtime() : 0ull;
   // Phase 5: certify, write, or queue.
   bool written = false, to_exact = false, to_lane = false;
   double d = 0.0;
@@ -1095,6 +1220,13 @@ __global__ void __launch_bounds__(256) k_nn4(NNLaunch a) {
   wave_append(to_exact, i, a.fb_count, a.fb_list);
   const bool covered = !(join && !(best <= u));
   wave_append_u(to_lane, i, covered ? u : __builtin_inf(), a.fb_count + 1, a.fb_list2, a.fb_u2);
+  if (a.dbg && lane == 0) {
+    const unsigned long long t_p5 = __builtin_amdgcn_s_memtime();
+    atomicAdd(&a.dbg[16], t_p2 - t_p0);
+    atomicAdd(&a.dbg[17], t_p3 - t_p2);
+    atomicAdd(&a.dbg[18], t_p4 - t_p3);
+    atomicAdd(&a.dbg[19], t_p5 - t_p4);
+  }
   if (!a.part) return;
   __syncthreads();
   double* red = reinterpret_cast<double*>(lds_stack);
@@ -1192,15 +1324,15 @@ __global__ void __launch_bounds__(64) k_nn_ball(NNLaunch a) {
           }
         }
         const int lcnt = (has && leaf) ? (int)(meta & ~kLeafBit) : 0;
-        const int lincl = wave_incl_scan(lcnt, lane);
-        const int ltot = __shfl(lincl, 63, kWave);
+        int ltot;
+        const int lincl = wave_incl_scan(lcnt, &ltot);
         const int lpos = npts + lincl - lcnt;
         if (lcnt > 0 && lpos + lcnt <= kBallPoints)
           for (int c = 0; c < lcnt; c++) plist[lpos + c] = first + c;
         npts += ltot;
         const int nch = __builtin_popcount(kids);
-        const int incl = wave_incl_scan(nch, lane);
-        const int tot = __shfl(incl, 63, kWave);
+        int tot;
+        const int incl = wave_incl_scan(nch, &tot);
         int off = nn + incl - nch;
         if (off + nch <= kBallFrontier) {
           const uint32_t mask = meta & 0xffu;
@@ -1547,9 +1679,21 @@ hipError_t launch_nn(const NNLaunch& a, hipStream_t s) {
   const unsigned grid = grid_for(a.n, bs);
   if (a.variant == 4 && !a.count) {
     // wave-cooperative search -> per-lane search for the rest -> exact fallback -> moments repair
-    const size_t shm4 = (size_t)(bs / kWave) * kWaveLdsBytes;
-    if (a.apply) hipLaunchKernelGGL((k_nn4<true>), dim3(grid), dim3(bs), shm4, s, a);
-    else hipLaunchKernelGGL((k_nn4<false>), dim3(grid), dim3(bs), shm4, s, a);
+    const int gl = (a.scan_group == 8 || a.scan_group == 16 || a.scan_group == 32) ? a.scan_group : 64;
+    const int pl = (gl == 64 && (a.wave_points == 512 || a.wave_points == 768)) ? a.wave_points : 1024;
+    const size_t shm4 = (size_t)(bs / kWave) * wave_lds_bytes(gl, pl);
+#define ICP_NN4(GL, PL)                                                                         \
+  do {                                                                                         \
+    if (a.apply) hipLaunchKernelGGL((k_nn4<true, GL, PL>), dim3(grid), dim3(bs), shm4, s, a);  \
+    else hipLaunchKernelGGL((k_nn4<false, GL, PL>), dim3(grid), dim3(bs), shm4, s, a);         \
+  } while (0)
+    if (gl == 8) ICP_NN4(8, 1024);
+    else if (gl == 16) ICP_NN4(16, 1024);
+    else if (gl == 32) ICP_NN4(32, 1024);
+    else if (pl == 512) ICP_NN4(64, 512);
+    else if (pl == 768) ICP_NN4(64, 768);
+    else ICP_NN4(64, 1024);
+#undef ICP_NN4
     if (a.ev_fast_done) (void)hipEventRecord(a.ev_fast_done, s);
     // the lists are short: 64-thread blocks spread them over every CU (latency-bound walks)
     const unsigned lgrid = (unsigned)((a.n + 63) / 64 < 4096 ? (a.n + 63) / 64 : 4096);

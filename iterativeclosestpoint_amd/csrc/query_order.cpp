@@ -1,6 +1,7 @@
 // query_order.cpp — order the source queries so that every 64 consecutive queries (one wave)
 // are spatially compact: a kd partition with 64-point buckets, each split on the longest axis
-// of the node's bounding box at a multiple of 64 near the median (std::nth_element). Buckets of
+// of the node's bounding box at a multiple of 64 near the median (std::nth_element), and each
+// 64-bucket split on down to `bucket` points (aligned lane groups of the search kernel). Buckets of
 // this partition have bounded aspect ratio, unlike Z-order runs, which jump across cell
 // boundaries; the wave-cooperative search scans ~the points of one bucket's neighbourhood.
 #include "query_order.h"
@@ -32,8 +33,11 @@ struct Part {
       int ax = 0;
       for (int a = 1; a < 3; a++)
         if (hi[a] - lo[a] > hi[ax] - lo[ax]) ax = a;
-      int64_t h = ((n / 2 + bucket - 1) / bucket) * bucket;
-      if (h >= n) h = n - bucket;
+      // splits at multiples of 64 (one wave) while the range is larger than a wave, then at
+      // multiples of `bucket` inside it: a wave's lanes form aligned kd sub-buckets
+      const int64_t unit = n > 64 ? 64 : bucket;
+      int64_t h = ((n / 2 + unit - 1) / unit) * unit;
+      if (h >= n) h = n - unit;
       const double* X = xyz;
       auto key = [X, ax](int32_t i) {
         const double v = X[3 * (int64_t)i + ax];
