@@ -13,7 +13,7 @@ import json
 import sys
 from collections import defaultdict
 
-KERNEL = "k_nn4<true>"
+KERNEL = "k_nn4<true"
 
 
 def rows(pattern):
