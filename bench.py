@@ -131,6 +131,7 @@ def main() -> int:
         dist.broadcast_object_list(uid, src=0)
         ctx.comm_init(world, rank, uid[0])
     setup_s = time.perf_counter() - t_setup
+    build_on_dev, build_ms = ctx.target_build_info()
 
     params = icp.params_default(max_iterations=args.warmup + args.steps + 1, tolerance=1e-6,
                                 flags=icp.FLAG_NO_EARLY_STOP)
@@ -216,6 +217,10 @@ def main() -> int:
             "roofline": {
                 "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                # the measured side: PMC HBM bytes per launch / the same launch time (the model above
+                # prices every node entry as an HBM read; most are L2/MALL hits, so frac can exceed 1)
+                "traffic_gbs": None if traffic is None else round(traffic / nn_avg_s / 1e9, 1),
+                "traffic_frac": None if traffic is None else round(traffic / nn_avg_s / 1e9 / HBM_PEAK_GBS, 4),
                 "kernel": "k_nn4 (fused transform + wave-cooperative certified octree NN + residual + block moments)",
                 "bytes_per_corr": round(b_corr, 1), "node_entries_per_query": round(v_mean, 3),
                 "leaf_points_per_query": round(p_mean, 3), "kernel_ms_avg": round(float(np.mean(nn_ms)), 4),
@@ -226,6 +231,7 @@ def main() -> int:
             },
             "cpu_baseline": cpu,
             "setup_s": round(setup_s, 2),
+            "octree_build": {"on_device": build_on_dev, "ms": round(build_ms, 2)},
             "final_rmse": res.final_rmse,
         }
         print(json.dumps(line), flush=True)

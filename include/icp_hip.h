@@ -80,11 +80,21 @@ void icp_hip_destroy(icp_hip_ctx* ctx);
 int icp_hip_get_unique_id(uint8_t out[ICP_HIP_UNIQUE_ID_BYTES]);
 int icp_hip_comm_init(icp_hip_ctx* ctx, int nranks, int rank, const uint8_t id[ICP_HIP_UNIQUE_ID_BYTES]);
 
-/* Build the reference octree of the target (AoS xyz, n points) on the host and upload it.
- * rules selects the initial best distance of findNearest. Non-finite target coordinates
- * and empty targets are rejected (ICP_HIP_EINVAL). */
+/* Build the reference octree of the target (AoS xyz, n points) and keep it in HBM. The tree is
+ * built on the device (max_depth <= 21; env ICP_OCTREE_BUILD=host forces the host builder) or on
+ * the host (deeper trees); both produce the same arrays bit for bit. rules selects the initial
+ * best distance of findNearest. Non-finite target coordinates and empty targets are rejected
+ * (ICP_HIP_EINVAL). Replaces Octree::Octree(points, max_pts, max_d), octree.cpp:41-126. */
 int icp_hip_set_target(icp_hip_ctx* ctx, const double* xyz, int64_t n, int max_points, int max_depth,
                        int rules);
+
+/* Which builder made the resident octree (1 = device) and the set_target time in ms. */
+int icp_hip_target_build_info(icp_hip_ctx* ctx, int32_t* on_device, double* build_ms);
+
+/* Copy the resident octree back in the layout of icp_octree_copy_nodes / _copy_points
+ * (icp_host.h); sizes from icp_hip_target_info (nodes) and the target size (points). */
+int icp_hip_copy_target(icp_hip_ctx* ctx, double* box6, int32_t* first, uint32_t* meta, int32_t* depth,
+                        double* xyz, int32_t* orig);
 
 /* Upload this rank's source shard (AoS xyz). Queries are reordered on the device along a
  * Morton curve for traversal coherence; every output is returned in the caller's order. */

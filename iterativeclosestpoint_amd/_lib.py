@@ -122,6 +122,8 @@ SIGNATURES = {
     "icp_hip_traversal_counts": (C.c_int, [_P, _D, _D]),
     "icp_hip_target_info": (C.c_int, [_P, C.POINTER(C.c_int64), C.POINTER(C.c_int64), _I32, _I32]),
     "icp_hip_last_timing": (C.c_int, [_P, _D, _D]),
+    "icp_hip_target_build_info": (C.c_int, [_P, _I32, _D]),
+    "icp_hip_copy_target": (C.c_int, [_P, _P, _P, _P, _P, _P, _P]),
     "icp_hip_synchronize": (C.c_int, [_P]),
     "icp_hip_last_error": (C.c_char_p, []),
     # icp_engine.h
@@ -258,6 +260,7 @@ class Context:
     def set_target(self, xyz, max_points=10, max_depth=20, rules=RULES_ENGINE):
         xyz = _aos(xyz)
         _check(lib().icp_hip_set_target(self._h, _ptr(xyz), xyz.shape[0], max_points, max_depth, rules))
+        self._n_tgt = xyz.shape[0]
 
     def set_source(self, xyz):
         xyz = _aos(xyz)
@@ -302,6 +305,28 @@ class Context:
         md, lv = C.c_int32(), C.c_int32()
         _check(lib().icp_hip_target_info(self._h, C.byref(nn_), C.byref(nl), C.byref(md), C.byref(lv)))
         return {"n_nodes": nn_.value, "n_leaves": nl.value, "max_depth": md.value, "stack_levels": lv.value}
+
+    def target_build_info(self):
+        """(built on the device?, set_target milliseconds on the context stream)."""
+        od, ms = C.c_int32(), C.c_double()
+        _check(lib().icp_hip_target_build_info(self._h, C.byref(od), C.byref(ms)))
+        return bool(od.value), ms.value
+
+    def copy_target(self) -> dict:
+        """The resident octree, in the layout of octree_build() (host builder)."""
+        info = self.target_info()
+        nn_ = info["n_nodes"]
+        npts = self._n_tgt
+        box = np.empty((nn_, 6))
+        first = np.empty(nn_, np.int32)
+        meta = np.empty(nn_, np.uint32)
+        depth = np.empty(nn_, np.int32)
+        pts = np.empty((npts, 3))
+        orig = np.empty(npts, np.int32)
+        _check(lib().icp_hip_copy_target(self._h, _ptr(box), _ptr(first), _ptr(meta), _ptr(depth), _ptr(pts),
+                                         _ptr(orig)))
+        return {"box": box, "first": first, "meta": meta, "depth": depth, "pts": pts, "orig": orig,
+                "n_leaves": info["n_leaves"], "max_depth": info["max_depth"]}
 
     def last_timing(self):
         a, b = C.c_double(), C.c_double()

@@ -22,6 +22,7 @@
 #include "icp_ctx_internal.h"
 #include "kernels.h"
 #include "octree_build.h"
+#include "octree_gpu.h"
 #include "query_order.h"
 
 using namespace icp;
@@ -176,25 +177,99 @@ int icp_hip_set_target(icp_hip_ctx* c, const double* xyz, int64_t n, int max_poi
   if (!c || (!xyz && n > 0)) return fail(ICP_HIP_EINVAL, "null argument");
   if (n <= 0) return fail(ICP_HIP_EINVAL, "empty target cloud (icpengine.cpp:31-34 rejects it)");
   if (max_depth < 0 || max_depth > 60) return fail(ICP_HIP_EINVAL, "max_depth out of range [0, 60]");
-  FlatOctree t;
-  const char* why = nullptr;
-  if (!build_flat_octree(xyz, n, max_points, max_depth, &t, &why)) return fail(ICP_HIP_EINVAL, why ? why : "bad target");
+  if (n > (int64_t)0x7fffffff) return fail(ICP_HIP_EINVAL, "target size out of range (int32 indices, as the reference)");
   HIP_TRY(hipSetDevice(c->device));
   free_target(c);
-  HIP_TRY(dalloc(&c->nodes, t.nodes.size()));
-  HIP_TRY(dalloc(&c->pts, t.pts.size()));
-  HIP_TRY(hipMemcpyAsync(c->nodes, t.nodes.data(), t.nodes.size() * sizeof(NodeRec), hipMemcpyHostToDevice, c->stream));
-  HIP_TRY(hipMemcpyAsync(c->pts, t.pts.data(), t.pts.size() * sizeof(TgtPt), hipMemcpyHostToDevice, c->stream));
+  hipEvent_t e0 = c->ev_it0, e1 = c->ev_it1;
+  HIP_TRY(hipEventRecord(e0, c->stream));
+  const char* mode = std::getenv("ICP_OCTREE_BUILD");  // "host" forces the host builder (A/B, tests)
+  const bool on_device = max_depth <= kGpuBuildMaxDepth && !(mode && std::strcmp(mode, "host") == 0);
+  if (on_device) {
+    // device build straight from the uploaded AoS cloud (octree_gpu.hip)
+    double* d_xyz = nullptr;
+    HIP_TRY(dalloc(&d_xyz, 3 * (size_t)n));
+    hipError_t e = hipMemcpyAsync(d_xyz, xyz, 3 * sizeof(double) * n, hipMemcpyHostToDevice, c->stream);
+    if (e != hipSuccess) {
+      dfree(d_xyz);
+      return fail(ICP_HIP_EDEVICE, std::string("set_target upload: ") + hipGetErrorString(e));
+    }
+    GpuOctree t;
+    std::string why;
+    const int rc = gpu_build_octree(d_xyz, n, max_points, max_depth, c->stream, &t, &why);
+    dfree(d_xyz);
+    if (rc != 0)
+      return fail(rc == 1 ? ICP_HIP_EINVAL : rc == -2 ? ICP_HIP_ENOMEM : ICP_HIP_EDEVICE, why);
+    c->nodes = t.nodes;
+    c->pts = t.pts;
+    c->n_nodes = t.n_nodes;
+    c->n_leaves = t.n_leaves;
+    c->pos0 = t.pos_of_orig0;
+    c->max_depth = t.max_depth;
+    c->levels = t.max_inner_depth + 1 > 0 ? t.max_inner_depth + 1 : 1;
+  } else {
+    FlatOctree t;
+    const char* why = nullptr;
+    if (!build_flat_octree(xyz, n, max_points, max_depth, &t, &why)) return fail(ICP_HIP_EINVAL, why ? why : "bad target");
+    HIP_TRY(dalloc(&c->nodes, t.nodes.size()));
+    HIP_TRY(dalloc(&c->pts, t.pts.size()));
+    HIP_TRY(hipMemcpyAsync(c->nodes, t.nodes.data(), t.nodes.size() * sizeof(NodeRec), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->pts, t.pts.data(), t.pts.size() * sizeof(TgtPt), hipMemcpyHostToDevice, c->stream));
+    c->n_nodes = (int64_t)t.nodes.size();
+    c->n_leaves = t.n_leaves;
+    c->pos0 = t.pos_of_orig0;
+    c->max_depth = t.max_depth;
+    c->levels = t.max_inner_depth + 1 > 0 ? t.max_inner_depth + 1 : 1;
+  }
+  HIP_TRY(hipEventRecord(e1, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
-  c->n_nodes = (int64_t)t.nodes.size();
-  c->n_leaves = t.n_leaves;
+  float ms = 0.f;
+  (void)hipEventElapsedTime(&ms, e0, e1);
+  c->target_build_ms = ms;
+  c->target_on_device = on_device ? 1 : 0;
   c->n_tgt = n;
-  c->pos0 = t.pos_of_orig0;
-  c->max_depth = t.max_depth;
-  c->levels = t.max_inner_depth + 1 > 0 ? t.max_inner_depth + 1 : 1;
   c->init_best = (rules == ICP_RULES_CLI) ? 1e20 : DBL_MAX;  // icp_registration.cpp:201 / octree.cpp:180
   c->have_prev = false;
   c->have_results = false;
+  return ICP_HIP_OK;
+}
+
+int icp_hip_target_build_info(icp_hip_ctx* c, int32_t* on_device, double* build_ms) {
+  if (!c) return fail(ICP_HIP_EINVAL, "null context");
+  if (!c->nodes) return fail(ICP_HIP_ENOTREADY, "target not set");
+  if (on_device) *on_device = c->target_on_device;
+  if (build_ms) *build_ms = c->target_build_ms;
+  return ICP_HIP_OK;
+}
+
+int icp_hip_copy_target(icp_hip_ctx* c, double* box6, int32_t* first, uint32_t* meta, int32_t* depth, double* xyz,
+                        int32_t* orig) {
+  if (!c) return fail(ICP_HIP_EINVAL, "null context");
+  if (!c->nodes) return fail(ICP_HIP_ENOTREADY, "target not set");
+  HIP_TRY(hipSetDevice(c->device));
+  std::vector<NodeRec> nodes((size_t)c->n_nodes);
+  std::vector<TgtPt> pts((size_t)c->n_tgt);
+  HIP_TRY(hipMemcpyAsync(nodes.data(), c->nodes, nodes.size() * sizeof(NodeRec), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipMemcpyAsync(pts.data(), c->pts, pts.size() * sizeof(TgtPt), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  for (size_t i = 0; i < nodes.size(); i++) {
+    const NodeRec& r = nodes[i];
+    if (box6)
+      for (int k = 0; k < 3; k++) {
+        box6[6 * i + k] = r.lo[k];
+        box6[6 * i + 3 + k] = r.hi[k];
+      }
+    if (first) first[i] = r.first;
+    if (meta) meta[i] = r.meta;
+    if (depth) depth[i] = r.depth;
+  }
+  for (size_t i = 0; i < pts.size(); i++) {
+    if (xyz) {
+      xyz[3 * i] = pts[i].x;
+      xyz[3 * i + 1] = pts[i].y;
+      xyz[3 * i + 2] = pts[i].z;
+    }
+    if (orig) orig[i] = pts[i].orig;
+  }
   return ICP_HIP_OK;
 }
 

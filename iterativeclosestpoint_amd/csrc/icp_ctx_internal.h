@@ -22,6 +22,8 @@ struct icp_hip_ctx {
   int64_t n_nodes = 0, n_leaves = 0, n_tgt = 0;
   int32_t pos0 = 0, max_depth = -1, levels = 1;
   double init_best = 1.7976931348623157e308;
+  int target_on_device = 0;      // octree built on the device (octree_gpu.hip) or on the host
+  double target_build_ms = 0.0;  // set_target wall time on the stream (upload + build)
 
   // this rank's source shard, Morton order (perm[k] = caller index of slot k)
   int64_t n_src = 0;
