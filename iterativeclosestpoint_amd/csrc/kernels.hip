@@ -856,6 +856,26 @@ __host__ __device__ constexpr int wave_lds_bytes(int gl, int pl) {
 }
 static_assert(2 * kWaveFrontier * 4 >= 64 * 32, "staging area aliases the frontier buffers");
 
+// Lower bound of fl64(d2) of every point whose fp32 squared distance (scan of k_nn4) is >= s32.
+// Coordinates are offsets from B's centre, |offset| <= ext for points and joined queries. With
+// u = 2^-24: each fp32 offset differs from the exact one by <= ext (u + 2^-53) =: ext k; the fp32
+// difference dx' = (p' - q')(1 + e), |e| <= u, so |dx' - dx| <= 2 ext k + u |dx| + ..., and over three
+// axes |‖d'‖ - D| <= e_abs + u D with e_abs = sqrt(3) 2 ext k (1 + u). The fp32 sum of squares
+// (one mul, two fma) is ‖d'‖^2 (1 + t), |t| <= (1 + u)^3 - 1, plus <= 3 2^-126 of underflow. Hence
+// D >= (sqrt((s32 - 2^-120) / (1 + 3.0001 u)) - e_abs) / (1 + u), and fl64(d2) >= D^2 (1 - 5 2^-53).
+// Every step below rounds towards the bound by an explicit 2^-50 margin.
+__device__ __forceinline__ double scan32_lower_bound(float s32, double ext) {
+  if (!(s32 < __builtin_inff())) return __builtin_inf();
+  const double u = 0x1p-24;
+  const double e_abs = 1.7320509 * 2.0 * ext * (u * (1.0 + 0x1p-20)) * (1.0 + u) * (1.0 + 0x1p-40);
+  double n2 = ((double)s32 - 0x1p-120) / (1.0 + 3.0001 * u);
+  if (!(n2 > 0.0)) return 0.0;
+  const double n = __builtin_sqrt(n2) * (1.0 - 0x1p-50);
+  double d = (n - e_abs) / (1.0 + u) * (1.0 - 0x1p-50);
+  if (!(d > 0.0)) return 0.0;
+  return d * d * (1.0 - 0x1p-48);
+}
+
 __device__ __forceinline__ void wave_lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
 
@@ -1080,7 +1100,79 @@ __global__ void __launch_bounds__(256) k_nn4(NNLaunch a) {
   int32_t bpos = -1;
   const int npts = nleaf;
   int scanned_pts = 0;
-  if (GL == 64 && __ballot(join) != 0 && npts > 0) {
+  // fp32 filter scan (GL = 64): the staged points and the joined queries lie in B, so relative
+  // to B's centre o every coordinate is at most A in magnitude and an fp32 offset carries an
+  // absolute error of at most ~A 2^-24. The wave tracks, per lane, the two smallest fp32 squared
+  // distances s1 <= s2 and the position of s1's point; that point's fp64 distance (the
+  // reference arithmetic) is recomputed and the certificate uses a rigorous lower bound of every
+  // other point's fp64 distance derived from s2 (error analysis at scan32_lower_bound). A wave
+  // where any joined lane cannot be certified this way redoes the scan in fp64 below.
+  bool need64 = GL == 64 && __ballot(join) != 0 && npts > 0;
+  if (GL == 64 && a.scan32 && need64) {
+    const double ocx = (blx + bhx) * 0.5, ocy = (bly + bhy) * 0.5, ocz = (blz + bhz) * 0.5;
+    const double ext = dmax_(dmax_(dmax_(bhx - ocx, ocx - blx), dmax_(bhy - ocy, ocy - bly)),
+                             dmax_(bhz - ocz, ocz - blz)) * (1.0 + 0x1p-40);
+    if (ext >= 0x1p-40 && ext <= 0x1p60) {
+      const float qx32 = (float)(qx - ocx), qy32 = (float)(qy - ocy), qz32 = (float)(qz - ocz);
+      float4* stage32 = reinterpret_cast<float4*>(wl);
+      float s1 = __builtin_inff(), s2 = __builtin_inff();
+      int32_t p1 = -1;
+      wave_lds_fence();
+      double4 nxtp = make_double4(0.0, 0.0, 0.0, 0.0);
+      if (lane < npts) {
+        const int32_t g = plist[lane];
+        const TgtPt* p = a.pts + g;
+        const double2 xy = *reinterpret_cast<const double2*>(&p->x);
+        nxtp = make_double4(xy.x, xy.y, p->z, __longlong_as_double((long long)g));
+      }
+      for (int base = 0; base < npts; base += 64) {
+        const bool nin = base + lane < npts && nxtp.x >= blx && nxtp.x <= bhx && nxtp.y >= bly && nxtp.y <= bhy &&
+                         nxtp.z >= blz && nxtp.z <= bhz;
+        const unsigned long long im = __ballot(nin);
+        const int slot = __builtin_amdgcn_mbcnt_hi((uint32_t)(im >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)im, 0));
+        const float4 v = make_float4((float)(nxtp.x - ocx), (float)(nxtp.y - ocy), (float)(nxtp.z - ocz),
+                                     __int_as_float((int)__double_as_longlong(nxtp.w)));
+        wave_lds_fence();  // previous chunk's reads are done before overwriting the staging slots
+        if (nin) stage32[slot] = v;
+        wave_lds_fence();
+        const int nb = base + 64;
+        if (nb + lane < npts) {
+          const int32_t g = plist[nb + lane];
+          const TgtPt* p = a.pts + g;
+          const double2 xy = *reinterpret_cast<const double2*>(&p->x);
+          nxtp = make_double4(xy.x, xy.y, p->z, __longlong_as_double((long long)g));
+        }
+        const int m = __popcll(im);
+        scanned_pts += m;
+        for (int k = 0; k < m; k++) {
+          const float4 pt = stage32[k];
+          const float dx = pt.x - qx32, dy = pt.y - qy32, dz = pt.z - qz32;
+          const float sq = __builtin_fmaf(dz, dz, __builtin_fmaf(dy, dy, dx * dx));
+          const bool lt = sq < s1;
+          s2 = __builtin_amdgcn_fmed3f(s1, s2, sq);
+          s1 = lt ? sq : s1;
+          p1 = lt ? __float_as_int(pt.w) : p1;
+        }
+      }
+      // fp64 distance of the fp32 winner, exactly as the leaf scan computes it (octree.cpp:139-144)
+      double b64 = __builtin_inf();
+      if (join && p1 >= 0) {
+        const TgtPt* p = a.pts + p1;
+        const double dx = p->x - qx, dy = p->y - qy, dz = p->z - qz;
+        b64 = dx * dx + dy * dy + dz * dz;
+      }
+      const double lb2 = scan32_lower_bound(s2, ext);
+      // a lane whose fp32 winner is not within its guess goes to the per-lane search either way
+      const bool ok = !join || p1 < 0 || !(b64 <= u) || certified(b64, lb2, a.init_best);
+      if (__ballot(!ok) == 0) {
+        best = b64;
+        second = lb2;
+        bpos = p1;
+        need64 = false;
+      }
+    }
+  }
+  if (GL == 64 && need64) {
     // Points outside B are farther than r from every joined lane (each ball lies in B), so
     // they can neither be a joined lane's nearest point nor sit in its certificate window.
     wave_lds_fence();

@@ -218,3 +218,66 @@ def test_fallback_share_small_on_scans(icp, gpu_ctx):
     gpu_ctx.set_source(src)
     st = gpu_ctx.iterate(None, 0, icp.RULES_ENGINE, 3.0)
     assert st.n_fallback <= 0.001 * len(src)
+
+
+def _with_env(env: dict, fn):
+    import os
+    old = {k: os.environ.get(k) for k in env}
+    try:
+        os.environ.update(env)
+        return fn()
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+@pytest.mark.parametrize("n", [300_000, 1_000_000])
+def test_scan32_matches_fp64_scan(icp, n):
+    """The fp32 filter scan of the wave search (fp64 winner + rigorous lower bound certificate)
+    returns exactly the fp64 scan's correspondences and residuals, iteration after iteration of
+    the real loop (previous-residual guesses, fused transform)."""
+    tgt, src, _ = icp.synth_pair(n)
+
+    def run():
+        out = []
+        with icp.Context(0) as ctx:
+            ctx.set_target(tgt, 10, 20, icp.RULES_ENGINE)
+            ctx.set_source(src)
+            T = None
+            for it in range(4):
+                st = ctx.iterate(T, it, icp.RULES_ENGINE, 3.0)
+                out.append(ctx.get_correspondences() + (st.n_fallback, st.n_ball_search))
+                T = icp.best_fit_from_stats(st)
+        return out
+
+    a = _with_env({"ICP_SCAN32": "1"}, run)
+    b = _with_env({"ICP_SCAN32": "0"}, run)
+    for (ia, da, fa, ba), (ib, db, fb, bb) in zip(a, b):
+        np.testing.assert_array_equal(ia, ib)
+        np.testing.assert_array_equal(da, db)
+        assert fa == fb and ba == bb
+
+
+def test_scan32_ties_and_self_queries(icp, oracle, golden_nn):
+    """Exact ties (lattice, duplicates) and zero distances (queries on target points) under the
+    fp32 filter: identical to the reference-order kernel."""
+    rng = np.random.default_rng(11)
+    for case in ("lattice", "duplicates", "gauss"):
+        t = golden_nn[f"{case}_target"]
+        q = np.concatenate([t[rng.integers(0, len(t), 3000)], golden_nn[f"{case}_query"]])
+
+        def run():
+            with icp.Context(0) as ctx:
+                ctx.set_target(t, 10, 20, icp.RULES_CLI)
+                ctx.set_source(q)
+                ctx.iterate(None, 0, icp.RULES_CLI, 3.0)
+                ctx.iterate(np.eye(4), 1, icp.RULES_CLI, 3.0)  # second pass: previous-residual guesses
+                return ctx.get_correspondences()
+
+        idx, d = _with_env({"ICP_SCAN32": "1"}, run)
+        oidx, od = oracle.OracleTree(t).nn(q, init_best=1e20)
+        np.testing.assert_array_equal(idx, oidx)
+        np.testing.assert_array_equal(d, od)

@@ -22,7 +22,7 @@ for v in (1, 2, 3, 4):
     agg = collections.defaultdict(float); cnt = collections.defaultdict(set)
     for f in glob.glob(f"gpurun_out/sq/v{v}_p*/**/*counter_collection.csv", recursive=True):
         for r in csv.DictReader(open(f)):
-            if "k_nn4<true>" in r["Kernel_Name"]:
+            if "k_nn4<true" in r["Kernel_Name"]:
                 agg[r["Counter_Name"]] += float(r["Counter_Value"]); cnt[r["Counter_Name"]].add(r["Dispatch_Id"])
     print(f"variant {v}:")
     for k in sorted(agg): print(f"  {k:32s} {agg[k]/max(1,len(cnt[k])):.4g}")
