@@ -109,6 +109,7 @@ int icp_hip_create(icp_hip_ctx** out, int device) {
   if (const char* v = std::getenv("ICP_SCAN_GROUP")) c->scan_group = std::atoi(v);
   if (const char* v = std::getenv("ICP_WAVE_POINTS")) c->wave_points = std::atoi(v);
   if (const char* v = std::getenv("ICP_SCAN32")) c->scan32 = std::atoi(v);
+  if (const char* v = std::getenv("ICP_LCA")) c->lca_descent = std::atoi(v);
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
     delete c;
     return fail(ICP_HIP_EDEVICE, "hipStreamCreate failed");
@@ -346,6 +347,7 @@ int icp_hip_iterate(icp_hip_ctx* c, const double* T_apply, int iter, int rules, 
   a.scan_group = c->scan_group;
   a.wave_points = c->wave_points;
   a.scan32 = c->scan32;
+  a.lca_descent = c->lca_descent;
   a.apply = T_apply ? 1 : 0;
   if (T_apply)
     for (int k = 0; k < 12; k++) a.T[k] = T_apply[k];
@@ -512,6 +514,7 @@ int icp_hip_nn(icp_hip_ctx* c, const double* q, int64_t n, int32_t* idx_out, dou
   a.scan_group = c->scan_group;
   a.wave_points = c->wave_points;
   a.scan32 = c->scan32;
+  a.lca_descent = c->lca_descent;
     int32_t* fbl = nullptr;
     double* fbu = nullptr;
     if (e == hipSuccess) e = dalloc(&fbl, 3 * (size_t)n);
@@ -563,6 +566,7 @@ int icp_hip_traversal_counts(icp_hip_ctx* c, double* mean_entries, double* mean_
   a.scan_group = c->scan_group;
   a.wave_points = c->wave_points;
   a.scan32 = c->scan32;
+  a.lca_descent = c->lca_descent;
   a.count = 1;
   HIP_TRY(launch_nn(a, c->stream));
   unsigned long long h[2] = {0, 0};

@@ -14,6 +14,7 @@ struct icp_hip_ctx {
   int scan_group = 64; // lanes per scan group of the wave search (ICP_SCAN_GROUP env: 8/16/32/64)
   int wave_points = 1024; // candidate-list capacity per wave (ICP_WAVE_POINTS env: 512/768/1024)
   int scan32 = 1;         // fp32 filter scan in the wave search (ICP_SCAN32=0: fp64 scan)
+  int lca_descent = 1;    // uniform descent before the wave's breadth-first walk (ICP_LCA=0: off)
   hipStream_t stream = nullptr;
   hipEvent_t ev_it0 = nullptr, ev_it1 = nullptr, ev_nn0 = nullptr, ev_nn1 = nullptr;
 

@@ -50,6 +50,7 @@ struct NNLaunch {
   int scan_group;          // variant 4: lanes per scan group (8, 16, 32 or 64 = whole wave)
   int wave_points;         // variant 4: candidate-list capacity per wave (512, 768 or 1024)
   int scan32;              // variant 4: fp32 filter scan with fp64 certification (0: fp64 scan)
+  int lca_descent;         // variant 4: wave-uniform descent to the deepest node covering B first
   unsigned long long* dbg; // optional diagnostics of the wave-cooperative search (ICP_NN_DEBUG)
 };
 

@@ -847,14 +847,15 @@ __global__ void __launch_bounds__(256) k_moments_fix(NNLaunch a, int part_size, 
 // join (outliers: far from the surface, or a wave whose candidate set overflows LDS) are queued
 // for the per-lane certified search (k_nn3_list); uncertified ones for the exact DFS.
 
-constexpr int kWaveFrontier = 256;  // node ids per frontier buffer (two buffers)
+constexpr int kWaveQueue = 256;     // node ids in the walk's circular work queue
 constexpr int kMaxGroups = 8;       // lane groups of the scan (GL = 8 lanes at the finest)
-// per wave: two frontier buffers (reused as the 64-point staging area once the walk is done),
-// the candidate list, the group boxes and the group index lists
+// per wave: the walk's work queue (reused as the staging area once the walk is done: 64 fp32
+// points or 32 fp64 points), the candidate list, the group boxes and the group index lists.
+// 1 KB + 4 KB at PL = 1024: 20 KB per 4-wave block, 8 blocks (8 waves per SIMD) per CU.
 __host__ __device__ constexpr int wave_lds_bytes(int gl, int pl) {
-  return 2 * kWaveFrontier * 4 + pl * 4 + (gl < 64 ? kMaxGroups * 64 * 2 : 0);
+  return kWaveQueue * 4 + pl * 4 + (gl < 64 ? kMaxGroups * 64 * 2 + 64 * 32 : 0);
 }
-static_assert(2 * kWaveFrontier * 4 >= 64 * 32, "staging area aliases the frontier buffers");
+static_assert(kWaveQueue * 4 >= 64 * 16 && kWaveQueue * 4 >= 32 * 32, "staging area aliases the queue");
 
 // Lower bound of fl64(d2) of every point whose fp32 squared distance (scan of k_nn4) is >= s32.
 // Coordinates are offsets from B's centre, |offset| <= ext for points and joined queries. With
@@ -884,7 +885,7 @@ __device__ __forceinline__ void wave_lds_fence() { asm volatile("s_waitcnt lgkmc
 // B_g (union of its joined lanes' balls, inside B); a lane scans only the staged points of its
 // group's box, the groups in parallel, so the lockstep loop runs max_g |B_g ∩ chunk| times.
 template <bool APPLY, int GL, int PL>
-__global__ void __launch_bounds__(256) k_nn4(NNLaunch a) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) k_nn4(NNLaunch a) {
   static_assert(GL == 64 || (GL >= 8 && 64 % GL == 0), "lane group size");
   constexpr int G = 64 / GL;
   extern __shared__ __attribute__((aligned(16))) unsigned long long lds_stack[];
@@ -892,12 +893,13 @@ __global__ void __launch_bounds__(256) k_nn4(NNLaunch a) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const bool active = i < a.n;
   unsigned char* wl = reinterpret_cast<unsigned char*>(lds_stack) + wv * wave_lds_bytes(GL, PL);
-  int32_t* fr0 = reinterpret_cast<int32_t*>(wl);
-  int32_t* fr1 = fr0 + kWaveFrontier;
+  int32_t* queue = reinterpret_cast<int32_t*>(wl);
   double4* stage = reinterpret_cast<double4*>(wl);                  // after the walk only
-  int32_t* plist = fr1 + kWaveFrontier;                             // candidate points
+  int32_t* plist = queue + kWaveQueue;                              // candidate points
   double* gbox = reinterpret_cast<double*>(plist + PL);    // G x 8 doubles
   unsigned char* gidx = reinterpret_cast<unsigned char*>(gbox + 8 * kMaxGroups);  // G x 64
+  // GL < 64: a full 64-point fp64 staging area of its own, after the group lists
+  if constexpr (GL < 64) stage = reinterpret_cast<double4*>(gidx + kMaxGroups * 64);
 
   double qx = 0.0, qy = 0.0, qz = 0.0, ox = 0.0, oy = 0.0, oz = 0.0;
   if (active) {
@@ -1012,76 +1014,96 @@ __global__ void __launch_bounds__(256) k_nn4(NNLaunch a) {
   int nleaf = 0;
   bool overflow = false;
   if (__ballot(join) != 0) {
-    int nf = 1;
-    int32_t* cur = fr0;
-    int32_t* nxt = fr1;
-    if (lane == 0) cur[0] = 0;
-    wave_lds_fence();
-    while (nf > 0) {
-      int nn = 0;
-      for (int base = 0; base < nf; base += 64) {
-        const int j = base + lane;
-        const bool has = j < nf;
-        // frontier nodes already meet B (tested by their parent; the root always does)
-        bool leaf = false, inner = false;
-        int32_t first = 0;
-        uint32_t meta = 0, kids = 0;
-        if (has) {
-          const NodeRec* rr = a.nodes + cur[j];
-          const int2 topo = *reinterpret_cast<const int2*>(&rr->first);
-          first = topo.x;
-          meta = (uint32_t)topo.y;
-          leaf = (meta & kLeafBit) != 0;
-          inner = !leaf;
-          if (inner) {
-            const double2 l01 = *reinterpret_cast<const double2*>(&rr->lo[0]);
-            const double2 l2h0 = *reinterpret_cast<const double2*>(&rr->lo[2]);
-            const double2 h12 = *reinterpret_cast<const double2*>(&rr->hi[1]);
-            const double lx = l01.x, ly = l01.y, lz = l2h0.x, hx = l2h0.y, hy = h12.x, hz = h12.y;
-            const double mx = (lx + hx) / 2, my = (ly + hy) / 2, mz = (lz + hz) / 2;
-            // child o spans [lo or mid, mid or hi] per axis (octree.cpp:115-120)
-            const bool x0 = lx <= bhx && mx >= blx, x1 = mx <= bhx && hx >= blx;
-            const bool y0 = ly <= bhy && my >= bly, y1 = my <= bhy && hy >= bly;
-            const bool z0 = lz <= bhz && mz >= blz, z1 = mz <= bhz && hz >= blz;
-            const uint32_t mask = meta & 0xffu;
+    // Wave-uniform descent to the deepest node that holds every leaf meeting B: follow the
+    // only child meeting B while there is exactly one (the top levels of the walk, where a
+    // whole 64-lane round would test a single node). All values here are wave-uniform.
+    int32_t start = 0;
+    if (a.lca_descent) {
+      while (true) {
+        const NodeRec* rr = a.nodes + start;
+        const int2 topo = *reinterpret_cast<const int2*>(&rr->first);
+        const uint32_t meta = (uint32_t)topo.y;
+        if (meta & kLeafBit) break;
+        const double lx = rr->lo[0], ly = rr->lo[1], lz = rr->lo[2], hx = rr->hi[0], hy = rr->hi[1], hz = rr->hi[2];
+        const double mx = (lx + hx) / 2, my = (ly + hy) / 2, mz = (lz + hz) / 2;
+        const bool x0 = lx <= bhx && mx >= blx, x1 = mx <= bhx && hx >= blx;
+        const bool y0 = ly <= bhy && my >= bly, y1 = my <= bhy && hy >= bly;
+        const bool z0 = lz <= bhz && mz >= blz, z1 = mz <= bhz && hz >= blz;
+        const uint32_t mask = meta & 0xffu;
+        uint32_t kids = 0;
 #pragma unroll
-            for (int o = 0; o < 8; o++) {
-              const bool hit = ((o & 1) ? x1 : x0) && ((o & 2) ? y1 : y0) && ((o & 4) ? z1 : z0);
-              kids |= (hit && ((mask >> o) & 1u)) ? (1u << o) : 0u;
-            }
-          }
+        for (int o = 0; o < 8; o++) {
+          const bool hit = ((o & 1) ? x1 : x0) && ((o & 2) ? y1 : y0) && ((o & 4) ? z1 : z0);
+          kids |= (hit && ((mask >> o) & 1u)) ? (1u << o) : 0u;
         }
-        // a leaf contributes its points (contiguous in leaf order) to the candidate list
-        const int lcnt = (has && leaf) ? (int)(meta & ~kLeafBit) : 0;
-        int ltot;
-        const int lincl = wave_incl_scan(lcnt, &ltot);
-        const int lpos = nleaf + lincl - lcnt;
-        if (lcnt > 0 && lpos + lcnt <= PL)
-          for (int c = 0; c < lcnt; c++) plist[lpos + c] = first + c;
-        nleaf += ltot;
-        const int nch = __builtin_popcount(kids);
-        int tot;
-        const int incl = wave_incl_scan(nch, &tot);
-        int off = nn + incl - nch;
-        if (off + nch <= kWaveFrontier) {
-          const uint32_t mask = meta & 0xffu;
-          uint32_t kk = kids;
-          while (kk) {
-            const uint32_t o = (uint32_t)__builtin_ctz(kk);
-            kk &= kk - 1u;
-            nxt[off++] = first + __builtin_popcount(mask & ((1u << o) - 1u));
-          }
-        }
-        nn += tot;
+        kids = (uint32_t)__builtin_amdgcn_readfirstlane((int)kids);
+        if (__builtin_popcount(kids) != 1) break;
+        const uint32_t o = (uint32_t)__builtin_ctz(kids);
+        start = __builtin_amdgcn_readfirstlane(topo.x + __builtin_popcount(mask & ((1u << o) - 1u)));
       }
-      if (nleaf > PL || nn > kWaveFrontier) {
+    }
+    // Work queue (circular, kWaveQueue entries): every batch takes up to 64 queued nodes, which
+    // already meet B (tested by their parent; the start node by the descent), appends the points
+    // of its leaves to the candidate list and its children meeting B to the queue's tail.
+    int head = 0, tail = 1;
+    if (lane == 0) queue[0] = start;
+    wave_lds_fence();
+    while (head < tail) {
+      const int batch = tail - head < 64 ? tail - head : 64;
+      const bool has = lane < batch;
+      bool leaf = false;
+      int32_t first = 0;
+      uint32_t meta = 0, kids = 0;
+      if (has) {
+        const NodeRec* rr = a.nodes + queue[(head + lane) & (kWaveQueue - 1)];
+        const int2 topo = *reinterpret_cast<const int2*>(&rr->first);
+        first = topo.x;
+        meta = (uint32_t)topo.y;
+        leaf = (meta & kLeafBit) != 0;
+        if (!leaf) {
+          const double2 l01 = *reinterpret_cast<const double2*>(&rr->lo[0]);
+          const double2 l2h0 = *reinterpret_cast<const double2*>(&rr->lo[2]);
+          const double2 h12 = *reinterpret_cast<const double2*>(&rr->hi[1]);
+          const double lx = l01.x, ly = l01.y, lz = l2h0.x, hx = l2h0.y, hy = h12.x, hz = h12.y;
+          const double mx = (lx + hx) / 2, my = (ly + hy) / 2, mz = (lz + hz) / 2;
+          // child o spans [lo or mid, mid or hi] per axis (octree.cpp:115-120)
+          const bool x0 = lx <= bhx && mx >= blx, x1 = mx <= bhx && hx >= blx;
+          const bool y0 = ly <= bhy && my >= bly, y1 = my <= bhy && hy >= bly;
+          const bool z0 = lz <= bhz && mz >= blz, z1 = mz <= bhz && hz >= blz;
+          const uint32_t mask = meta & 0xffu;
+#pragma unroll
+          for (int o = 0; o < 8; o++) {
+            const bool hit = ((o & 1) ? x1 : x0) && ((o & 2) ? y1 : y0) && ((o & 4) ? z1 : z0);
+            kids |= (hit && ((mask >> o) & 1u)) ? (1u << o) : 0u;
+          }
+        }
+      }
+      // a leaf contributes its points (contiguous in leaf order) to the candidate list
+      const int lcnt = (has && leaf) ? (int)(meta & ~kLeafBit) : 0;
+      int ltot;
+      const int lincl = wave_incl_scan(lcnt, &ltot);
+      const int lpos = nleaf + lincl - lcnt;
+      if (lcnt > 0 && lpos + lcnt <= PL)
+        for (int c = 0; c < lcnt; c++) plist[lpos + c] = first + c;
+      nleaf += ltot;
+      const int nch = __builtin_popcount(kids);
+      int tot;
+      const int incl = wave_incl_scan(nch, &tot);
+      head += batch;
+      // the unprocessed entries [head, tail) must survive the appends
+      if (nleaf > PL || tail + tot - head > kWaveQueue) {
         overflow = true;
         break;
       }
-      int32_t* t = cur;
-      cur = nxt;
-      nxt = t;
-      nf = nn;
+      int off = tail + incl - nch;
+      const uint32_t mask = meta & 0xffu;
+      uint32_t kk = kids;
+      while (kk) {
+        const uint32_t o = (uint32_t)__builtin_ctz(kk);
+        kk &= kk - 1u;
+        queue[(off++) & (kWaveQueue - 1)] = first + __builtin_popcount(mask & ((1u << o) - 1u));
+      }
+      tail += tot;
       if (a.dbg && lane == 0) atomicAdd(&a.dbg[5], 1ull);
       wave_lds_fence();
     }
@@ -1189,9 +1211,7 @@ __global__ void __launch_bounds__(256) k_nn4(NNLaunch a) {
             nxtp.z >= blz && nxtp.z <= bhz;
       const unsigned long long im = __ballot(nin);
       const int slot = __builtin_amdgcn_mbcnt_hi((uint32_t)(im >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)im, 0));
-      wave_lds_fence();  // previous chunk's reads are done before overwriting the staging slots
-      if (nin) stage[slot] = nxtp;
-      wave_lds_fence();
+      const double4 cur = nxtp;
       const int nb = base + 64;
       if (nb + lane < npts) {
         const int32_t g = plist[nb + lane];
@@ -1201,16 +1221,23 @@ __global__ void __launch_bounds__(256) k_nn4(NNLaunch a) {
       }
       const int m = __popcll(im);
       scanned_pts += m;
-      for (int k = 0; k < m; k++) {
-        const double4 pt = stage[k];
-        const double dx = pt.x - qx, dy = pt.y - qy, dz = pt.z - qz;
-        const double d2 = dx * dx + dy * dy + dz * dz;
-        if (d2 < best) {
-          second = best;
-          best = d2;
-          bpos = (int32_t)__double_as_longlong(pt.w);
-        } else if (d2 < second) {
-          second = d2;
+      // the staging area holds 32 fp64 points: the chunk's in-B points in two halves
+      for (int h = 0; h < m; h += 32) {
+        wave_lds_fence();  // the previous half's reads are done before its slots are rewritten
+        if (nin && slot >= h && slot < h + 32) stage[slot - h] = cur;
+        wave_lds_fence();
+        const int mh = m - h < 32 ? m - h : 32;
+        for (int k = 0; k < mh; k++) {
+          const double4 pt = stage[k];
+          const double dx = pt.x - qx, dy = pt.y - qy, dz = pt.z - qz;
+          const double d2 = dx * dx + dy * dy + dz * dz;
+          if (d2 < best) {
+            second = best;
+            best = d2;
+            bpos = (int32_t)__double_as_longlong(pt.w);
+          } else if (d2 < second) {
+            second = d2;
+          }
         }
       }
     }

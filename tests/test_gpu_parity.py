@@ -234,8 +234,9 @@ def _with_env(env: dict, fn):
                 os.environ[k] = v
 
 
-@pytest.mark.parametrize("n", [300_000, 1_000_000])
-def test_scan32_matches_fp64_scan(icp, n):
+@pytest.mark.parametrize("n,env", [(300_000, {"ICP_SCAN32": "0"}), (1_000_000, {"ICP_SCAN32": "0"}),
+                                   (1_000_000, {"ICP_LCA": "0"}), (300_000, {"ICP_SCAN32": "0", "ICP_LCA": "0"})])
+def test_scan32_matches_fp64_scan(icp, n, env):
     """The fp32 filter scan of the wave search (fp64 winner + rigorous lower bound certificate)
     returns exactly the fp64 scan's correspondences and residuals, iteration after iteration of
     the real loop (previous-residual guesses, fused transform)."""
@@ -253,8 +254,8 @@ def test_scan32_matches_fp64_scan(icp, n):
                 T = icp.best_fit_from_stats(st)
         return out
 
-    a = _with_env({"ICP_SCAN32": "1"}, run)
-    b = _with_env({"ICP_SCAN32": "0"}, run)
+    a = run()
+    b = _with_env(env, run)
     for (ia, da, fa, ba), (ib, db, fb, bb) in zip(a, b):
         np.testing.assert_array_equal(ia, ib)
         np.testing.assert_array_equal(da, db)
