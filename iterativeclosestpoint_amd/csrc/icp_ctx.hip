@@ -83,6 +83,8 @@ static void free_source(icp_hip_ctx* c) {
 static void free_target(icp_hip_ctx* c) {
   dfree(c->nodes);
   dfree(c->pts);
+  dfree(c->cells);
+  c->cell_lmax = -1;
   c->n_nodes = 0;
   c->n_tgt = 0;
 }
@@ -110,6 +112,7 @@ int icp_hip_create(icp_hip_ctx** out, int device) {
   if (const char* v = std::getenv("ICP_WAVE_POINTS")) c->wave_points = std::atoi(v);
   if (const char* v = std::getenv("ICP_SCAN32")) c->scan32 = std::atoi(v);
   if (const char* v = std::getenv("ICP_LCA")) c->lca_descent = std::atoi(v);
+  if (const char* v = std::getenv("ICP_CELLS")) c->use_cells = std::atoi(v);
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
     delete c;
     return fail(ICP_HIP_EDEVICE, "hipStreamCreate failed");
@@ -221,6 +224,22 @@ int icp_hip_set_target(icp_hip_ctx* c, const double* xyz, int64_t n, int max_poi
     c->pos0 = t.pos_of_orig0;
     c->max_depth = t.max_depth;
     c->levels = t.max_inner_depth + 1 > 0 ? t.max_inner_depth + 1 : 1;
+  }
+  // root box (host copy: the kernels' cell arithmetic starts from it) and the cell tables
+  {
+    NodeRec root;
+    HIP_TRY(hipMemcpyAsync(&root, c->nodes, sizeof(NodeRec), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    for (int k = 0; k < 3; k++) {
+      c->root_box[k] = root.lo[k];
+      c->root_box[3 + k] = root.hi[k];
+    }
+  }
+  if (c->use_cells && c->n_nodes < ((int64_t)1 << 26)) {
+    const int lmax = cell_table_depth(c->n_leaves, c->levels - 1);
+    HIP_TRY(dalloc(&c->cells, (size_t)cell_table_entries(lmax)));
+    HIP_TRY(build_cell_tables(c->nodes, lmax, c->cells, c->stream));
+    c->cell_lmax = lmax;
   }
   HIP_TRY(hipEventRecord(e1, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
@@ -348,6 +367,12 @@ int icp_hip_iterate(icp_hip_ctx* c, const double* T_apply, int iter, int rules, 
   a.wave_points = c->wave_points;
   a.scan32 = c->scan32;
   a.lca_descent = c->lca_descent;
+  a.cells = c->cells;
+  a.cell_lmax = c->cell_lmax;
+  for (int k = 0; k < 3; k++) {
+    a.root_lo[k] = c->root_box[k];
+    a.root_hi[k] = c->root_box[3 + k];
+  }
   a.apply = T_apply ? 1 : 0;
   if (T_apply)
     for (int k = 0; k < 12; k++) a.T[k] = T_apply[k];
@@ -417,8 +442,11 @@ int icp_hip_iterate(icp_hip_ctx* c, const double* T_apply, int iter, int rules, 
     unsigned long long h[24];
     if (hipMemcpy(h, c->dbg, sizeof(h), hipMemcpyDeviceToHost) == hipSuccess) {
       const double w = h[0] ? (double)h[0] : 1.0;
-      std::fprintf(stderr, "[icp dbg] iter=%d wave clocks: guess+box=%.0f walk=%.0f scan=%.0f finish=%.0f\n", iter,
-                   (double)h[16] / w, (double)h[17] / w, (double)h[18] / w, (double)h[19] / w);
+      std::fprintf(stderr,
+                   "[icp dbg] iter=%d wave clocks: guess+box=%.0f descent=%.0f walk=%.0f scan=%.0f finish=%.0f "
+                   "descent_levels/wave=%.2f\n",
+                   iter, (double)h[16] / w, (double)h[20] / w, (double)h[17] / w, (double)h[18] / w,
+                   (double)h[19] / w, (double)h[21] / w);
       const double nl = c->last_lists[2] ? (double)c->last_lists[2] : 1.0;
       std::fprintf(stderr, "[icp dbg] iter=%d ball_list=%u ball_overflow=%llu ball_pts/query=%.1f lane_list=%u\n", iter,
                    c->last_lists[1], h[14], c->last_lists[1] ? (double)h[15] / c->last_lists[1] : 0.0,
@@ -515,6 +543,12 @@ int icp_hip_nn(icp_hip_ctx* c, const double* q, int64_t n, int32_t* idx_out, dou
   a.wave_points = c->wave_points;
   a.scan32 = c->scan32;
   a.lca_descent = c->lca_descent;
+  a.cells = c->cells;
+  a.cell_lmax = c->cell_lmax;
+  for (int k = 0; k < 3; k++) {
+    a.root_lo[k] = c->root_box[k];
+    a.root_hi[k] = c->root_box[3 + k];
+  }
     int32_t* fbl = nullptr;
     double* fbu = nullptr;
     if (e == hipSuccess) e = dalloc(&fbl, 3 * (size_t)n);
@@ -567,6 +601,12 @@ int icp_hip_traversal_counts(icp_hip_ctx* c, double* mean_entries, double* mean_
   a.wave_points = c->wave_points;
   a.scan32 = c->scan32;
   a.lca_descent = c->lca_descent;
+  a.cells = c->cells;
+  a.cell_lmax = c->cell_lmax;
+  for (int k = 0; k < 3; k++) {
+    a.root_lo[k] = c->root_box[k];
+    a.root_hi[k] = c->root_box[3 + k];
+  }
   a.count = 1;
   HIP_TRY(launch_nn(a, c->stream));
   unsigned long long h[2] = {0, 0};

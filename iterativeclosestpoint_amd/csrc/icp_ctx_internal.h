@@ -15,6 +15,7 @@ struct icp_hip_ctx {
   int wave_points = 1024; // candidate-list capacity per wave (ICP_WAVE_POINTS env: 512/768/1024)
   int scan32 = 1;         // fp32 filter scan in the wave search (ICP_SCAN32=0: fp64 scan)
   int lca_descent = 1;    // uniform descent before the wave's breadth-first walk (ICP_LCA=0: off)
+  int use_cells = 1;      // start the wave walk from the cell tables (ICP_CELLS=0: off)
   hipStream_t stream = nullptr;
   hipEvent_t ev_it0 = nullptr, ev_it1 = nullptr, ev_nn0 = nullptr, ev_nn1 = nullptr;
 
@@ -24,6 +25,9 @@ struct icp_hip_ctx {
   int64_t n_nodes = 0, n_leaves = 0, n_tgt = 0;
   int32_t pos0 = 0, max_depth = -1, levels = 1;
   double init_best = 1.7976931348623157e308;
+  int32_t* cells = nullptr;     // per-level cell tables of the octree (octree_gpu.h)
+  int cell_lmax = -1;
+  double root_box[6] = {0, 0, 0, 0, 0, 0};
   int target_on_device = 0;      // octree built on the device (octree_gpu.hip) or on the host
   double target_build_ms = 0.0;  // set_target wall time on the stream (upload + build)
 

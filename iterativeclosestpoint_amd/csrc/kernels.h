@@ -51,6 +51,9 @@ struct NNLaunch {
   int wave_points;         // variant 4: candidate-list capacity per wave (512, 768 or 1024)
   int scan32;              // variant 4: fp32 filter scan with fp64 certification (0: fp64 scan)
   int lca_descent;         // variant 4: wave-uniform descent to the deepest node covering B first
+  const int32_t* cells;    // variant 4: per-level cell tables (octree_gpu.h), null = not used
+  int cell_lmax;           // deepest table level
+  double root_lo[3], root_hi[3];  // root box (the octree's midpoint recursion starts here)
   unsigned long long* dbg; // optional diagnostics of the wave-cooperative search (ICP_NN_DEBUG)
 };
 

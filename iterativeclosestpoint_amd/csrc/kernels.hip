@@ -877,6 +877,16 @@ __device__ __forceinline__ double scan32_lower_bound(float s32, double ext) {
   return d * d * (1.0 - 0x1p-48);
 }
 
+// Bits 0..9 of v spread to bits 0, 3, 6, ... (one axis of an octant path prefix).
+__device__ __forceinline__ uint32_t spread3(uint32_t v) {
+  v &= 0x3ffu;
+  v = (v | (v << 16)) & 0x030000ffu;
+  v = (v | (v << 8)) & 0x0300f00fu;
+  v = (v | (v << 4)) & 0x030c30c3u;
+  v = (v | (v << 2)) & 0x09249249u;
+  return v;
+}
+
 __device__ __forceinline__ void wave_lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
 
@@ -1010,6 +1020,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
   }
 
   const unsigned long long t_p2 = a.dbg ? __builtin_amdgcn_s_memtime() : 0ull;
+  unsigned long long t_pd = t_p2;
   // Phase 3: cooperative breadth-first collection of the leaves meeting B.
   int nleaf = 0;
   bool overflow = false;
@@ -1018,7 +1029,59 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
     // only child meeting B while there is exactly one (the top levels of the walk, where a
     // whole 64-lane round would test a single node). All values here are wave-uniform.
     int32_t start = 0;
-    if (a.lca_descent) {
+    int tail = 1;
+    if (a.cells) {
+      // Start from the cell tables: the cells of level L (the octree's own midpoint grid) that
+      // B overlaps, one lane each. Per axis, the cell index of a coordinate is the bit path of
+      // its comparisons with the successive midpoints (x > mid goes high, octree.cpp:105-108),
+      // monotone in the coordinate, so B's cells are an index box [il, ih]^3 and every target
+      // point in B lies in one of them; the table gives the node holding all points of a cell
+      // (the depth-L node or the leaf above it; a leaf spanning several cells is queued once,
+      // from its first cell in the box).
+      int L = a.cell_lmax;
+      uint32_t path = 0;
+      if (lane < 6) {
+        const int ax = lane >> 1;
+        const double v = (lane & 1) ? (ax == 0 ? bhx : ax == 1 ? bhy : bhz) : (ax == 0 ? blx : ax == 1 ? bly : blz);
+        double lo = ax == 0 ? a.root_lo[0] : ax == 1 ? a.root_lo[1] : a.root_lo[2];
+        double hi = ax == 0 ? a.root_hi[0] : ax == 1 ? a.root_hi[1] : a.root_hi[2];
+        for (int l = 0; l < L; l++) {
+          const double m = (lo + hi) / 2;
+          const bool up = v > m;
+          path = 2u * path + (up ? 1u : 0u);
+          lo = up ? m : lo;
+          hi = up ? hi : m;
+        }
+      }
+      uint32_t ilx = (uint32_t)__builtin_amdgcn_readlane((int)path, 0), ihx = (uint32_t)__builtin_amdgcn_readlane((int)path, 1);
+      uint32_t ily = (uint32_t)__builtin_amdgcn_readlane((int)path, 2), ihy = (uint32_t)__builtin_amdgcn_readlane((int)path, 3);
+      uint32_t ilz = (uint32_t)__builtin_amdgcn_readlane((int)path, 4), ihz = (uint32_t)__builtin_amdgcn_readlane((int)path, 5);
+      while (L > 0 && (ihx - ilx + 1) * (ihy - ily + 1) * (ihz - ilz + 1) > 64) {
+        L--;
+        ilx >>= 1; ihx >>= 1; ily >>= 1; ihy >>= 1; ilz >>= 1; ihz >>= 1;
+      }
+      const uint32_t nx = ihx - ilx + 1, ny = ihy - ily + 1, nz = ihz - ilz + 1;
+      bool put = false;
+      int32_t node = 0;
+      if ((uint32_t)lane < nx * ny * nz) {
+        const uint32_t cx = ilx + (uint32_t)lane % nx, cy = ily + ((uint32_t)lane / nx) % ny,
+                       cz = ilz + (uint32_t)lane / (nx * ny);
+        const uint32_t prefix = spread3(cx) | (spread3(cy) << 1) | (spread3(cz) << 2);
+        const int32_t e = a.cells[(((int64_t)1 << (3 * L)) - 1) / 7 + prefix];
+        if (e >= 0) {
+          node = e >> 5;
+          const int sh = L - (e & 31);
+          const uint32_t fx = ((cx >> sh) << sh) > ilx ? ((cx >> sh) << sh) : ilx;
+          const uint32_t fy = ((cy >> sh) << sh) > ily ? ((cy >> sh) << sh) : ily;
+          const uint32_t fz = ((cz >> sh) << sh) > ilz ? ((cz >> sh) << sh) : ilz;
+          put = cx == fx && cy == fy && cz == fz;
+        }
+      }
+      const unsigned long long pm = __ballot(put);
+      if (put) queue[__builtin_amdgcn_mbcnt_hi((uint32_t)(pm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)pm, 0))] = node;
+      tail = __popcll(pm);
+      if (a.dbg && lane == 0) atomicAdd(&a.dbg[21], (unsigned long long)tail);
+    } else if (a.lca_descent) {
       while (true) {
         const NodeRec* rr = a.nodes + start;
         const int2 topo = *reinterpret_cast<const int2*>(&rr->first);
@@ -1040,22 +1103,24 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
         if (__builtin_popcount(kids) != 1) break;
         const uint32_t o = (uint32_t)__builtin_ctz(kids);
         start = __builtin_amdgcn_readfirstlane(topo.x + __builtin_popcount(mask & ((1u << o) - 1u)));
+        if (a.dbg && lane == 0) atomicAdd(&a.dbg[21], 1ull);
       }
     }
-    // Work queue (circular, kWaveQueue entries): every batch takes up to 64 queued nodes, which
-    // already meet B (tested by their parent; the start node by the descent), appends the points
-    // of its leaves to the candidate list and its children meeting B to the queue's tail.
-    int head = 0, tail = 1;
-    if (lane == 0) queue[0] = start;
+    if (a.dbg) t_pd = __builtin_amdgcn_s_memtime();
+    // Work stack (kWaveQueue entries): every batch pops up to 64 nodes, which already meet B
+    // (tested by their parent; the start nodes by the descent or the cell box), appends the
+    // points of its leaves to the candidate list and pushes its children meeting B. Popping the
+    // most recent nodes first keeps the live set small (depth-first in wave-wide batches).
+    if (!a.cells && lane == 0) queue[0] = start;
     wave_lds_fence();
-    while (head < tail) {
-      const int batch = tail - head < 64 ? tail - head : 64;
+    while (tail > 0) {
+      const int batch = tail < 64 ? tail : 64;
       const bool has = lane < batch;
       bool leaf = false;
       int32_t first = 0;
       uint32_t meta = 0, kids = 0;
       if (has) {
-        const NodeRec* rr = a.nodes + queue[(head + lane) & (kWaveQueue - 1)];
+        const NodeRec* rr = a.nodes + queue[tail - batch + lane];
         const int2 topo = *reinterpret_cast<const int2*>(&rr->first);
         first = topo.x;
         meta = (uint32_t)topo.y;
@@ -1089,9 +1154,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
       const int nch = __builtin_popcount(kids);
       int tot;
       const int incl = wave_incl_scan(nch, &tot);
-      head += batch;
-      // the unprocessed entries [head, tail) must survive the appends
-      if (nleaf > PL || tail + tot - head > kWaveQueue) {
+      tail -= batch;  // the popped entries are in registers; children overwrite them
+      if (nleaf > PL || tail + tot > kWaveQueue) {
         overflow = true;
         break;
       }
@@ -1101,7 +1165,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
       while (kk) {
         const uint32_t o = (uint32_t)__builtin_ctz(kk);
         kk &= kk - 1u;
-        queue[(off++) & (kWaveQueue - 1)] = first + __builtin_popcount(mask & ((1u << o) - 1u));
+        queue[off++] = first + __builtin_popcount(mask & ((1u << o) - 1u));
       }
       tail += tot;
       if (a.dbg && lane == 0) atomicAdd(&a.dbg[5], 1ull);
@@ -1342,7 +1406,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
   if (a.dbg && lane == 0) {
     const unsigned long long t_p5 = __builtin_amdgcn_s_memtime();
     atomicAdd(&a.dbg[16], t_p2 - t_p0);
-    atomicAdd(&a.dbg[17], t_p3 - t_p2);
+    atomicAdd(&a.dbg[17], t_p3 - t_pd);
+    atomicAdd(&a.dbg[20], t_pd - t_p2);
     atomicAdd(&a.dbg[18], t_p4 - t_p3);
     atomicAdd(&a.dbg[19], t_p5 - t_p4);
   }

@@ -27,4 +27,14 @@ struct GpuOctree {
 int gpu_build_octree(const double* xyz, int64_t n, int max_pts, int max_d, hipStream_t s, GpuOctree* out,
                      std::string* why);
 
+// Per-level cell tables (SURVEY.md §8 a5 acceleration, search side only): for every level
+// l <= lmax, 8^l int32 entries indexed by an l-level path prefix (the octant bits of the
+// octree's own midpoint splits, level 1 most significant), each = (node << 5) | depth of the
+// node holding all points of the cell (the depth-l node, or the leaf above it), -1 if empty.
+// Levels are stored back to back (offset of level l = (8^l - 1) / 7).
+int64_t cell_table_entries(int lmax);
+int64_t cell_table_offset(int l);
+int cell_table_depth(int64_t n_leaves, int max_inner_depth);
+hipError_t build_cell_tables(const NodeRec* nodes, int lmax, int32_t* tables, hipStream_t s);
+
 }  // namespace icp

@@ -348,6 +348,58 @@ struct Scratch {
   }
 };
 
+// Cell table of level L: entry e (an L-level path prefix, level 1 in the top 3 bits) = the
+// node holding every target point of that cell: the node at depth L, or the leaf above it, as
+// (node id << 5) | node depth; -1 when the cell holds no point (a child on the path is absent).
+__global__ void __launch_bounds__(kTB) k_cell_table(const NodeRec* __restrict__ nodes, int L, int64_t nent,
+                                                    int32_t* __restrict__ table) {
+  const int64_t e = blockIdx.x * (int64_t)kTB + threadIdx.x;
+  if (e >= nent) return;
+  int32_t node = 0;
+  int d = 0;
+  for (; d < L; d++) {
+    const int2 topo = *reinterpret_cast<const int2*>(&nodes[node].first);
+    const uint32_t meta = (uint32_t)topo.y;
+    if (meta & kLeafBit) break;
+    const uint32_t o = (uint32_t)(e >> (3 * (L - 1 - d))) & 7u;
+    if (!((meta >> o) & 1u)) {
+      node = -1;
+      break;
+    }
+    node = topo.x + __builtin_popcount(meta & 0xffu & ((1u << o) - 1u));
+  }
+  table[e] = node < 0 ? -1 : (int32_t)(((uint32_t)node << 5) | (uint32_t)d);
+}
+
+}  // namespace
+
+int64_t cell_table_entries(int lmax) {
+  int64_t tot = 0, w = 1;
+  for (int l = 0; l <= lmax; l++, w *= 8) tot += w;
+  return tot;
+}
+
+int64_t cell_table_offset(int l) { return l == 0 ? 0 : cell_table_entries(l - 1); }
+
+int cell_table_depth(int64_t n_leaves, int max_inner_depth) {
+  // about one cell per leaf at the deepest table level, at most 9 levels (153M entries)
+  int l = 1;
+  while (l < 9 && ((int64_t)1 << (3 * l)) < n_leaves) l++;
+  if (l > max_inner_depth + 1) l = max_inner_depth + 1;
+  return l < 0 ? 0 : l;
+}
+
+hipError_t build_cell_tables(const NodeRec* nodes, int lmax, int32_t* tables, hipStream_t s) {
+  for (int l = 0; l <= lmax; l++) {
+    const int64_t nent = (int64_t)1 << (3 * l);
+    hipLaunchKernelGGL(k_cell_table, dim3(grid_for(nent, kTB)), dim3(kTB), 0, s, nodes, l, nent,
+                       tables + cell_table_offset(l));
+  }
+  return hipGetLastError();
+}
+
+namespace {
+
 }  // namespace
 
 #define OCT_TRY(expr)                                      \

@@ -235,7 +235,8 @@ def _with_env(env: dict, fn):
 
 
 @pytest.mark.parametrize("n,env", [(300_000, {"ICP_SCAN32": "0"}), (1_000_000, {"ICP_SCAN32": "0"}),
-                                   (1_000_000, {"ICP_LCA": "0"}), (300_000, {"ICP_SCAN32": "0", "ICP_LCA": "0"})])
+                                   (1_000_000, {"ICP_LCA": "0"}), (300_000, {"ICP_SCAN32": "0", "ICP_LCA": "0"}),
+                                   (1_000_000, {"ICP_CELLS": "0"}), (300_000, {"ICP_CELLS": "0", "ICP_LCA": "0"})])
 def test_scan32_matches_fp64_scan(icp, n, env):
     """The fp32 filter scan of the wave search (fp64 winner + rigorous lower bound certificate)
     returns exactly the fp64 scan's correspondences and residuals, iteration after iteration of
@@ -259,7 +260,9 @@ def test_scan32_matches_fp64_scan(icp, n, env):
     for (ia, da, fa, ba), (ib, db, fb, bb) in zip(a, b):
         np.testing.assert_array_equal(ia, ib)
         np.testing.assert_array_equal(da, db)
-        assert fa == fb and ba == bb
+        assert fa == fb
+        if "ICP_CELLS" not in env:  # the same candidate sets (cell starts change which waves overflow)
+            assert ba == bb
 
 
 def test_scan32_ties_and_self_queries(icp, oracle, golden_nn):
