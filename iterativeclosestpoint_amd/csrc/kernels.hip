@@ -890,6 +890,61 @@ __device__ __forceinline__ uint32_t spread3(uint32_t v) {
 __device__ __forceinline__ void wave_lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
 
+// Start nodes of a box query from the cell tables: the cells of level L (the octree's own
+// midpoint grid) that the box [bl, bh] overlaps, one lane each. Per axis, the cell index of a
+// coordinate is the bit path of its comparisons with the successive midpoints (x > mid goes
+// high, octree.cpp:105-108), monotone in the coordinate, so the box's cells are an index box
+// [il, ih]^3, every one of them meets the box, and every target point inside the box lies in
+// one of them; the table gives the node holding all points of a cell (the depth-L node or the
+// leaf above it; a leaf spanning several cells is queued once, from its first cell in the box).
+// L is the deepest table level at which the box spans at most 64 cells. Writes the start nodes
+// to out[0 .. count) and returns count (wave-uniform). Every lane of the wave must call it.
+__device__ __forceinline__ int cell_starts(const NNLaunch& a, double blx, double bly, double blz, double bhx,
+                                           double bhy, double bhz, int lane, int32_t* out) {
+  int L = a.cell_lmax;
+  uint32_t path = 0;
+  if (lane < 6) {
+    const int ax = lane >> 1;
+    const double v = (lane & 1) ? (ax == 0 ? bhx : ax == 1 ? bhy : bhz) : (ax == 0 ? blx : ax == 1 ? bly : blz);
+    double lo = ax == 0 ? a.root_lo[0] : ax == 1 ? a.root_lo[1] : a.root_lo[2];
+    double hi = ax == 0 ? a.root_hi[0] : ax == 1 ? a.root_hi[1] : a.root_hi[2];
+    for (int l = 0; l < L; l++) {
+      const double m = (lo + hi) / 2;
+      const bool up = v > m;
+      path = 2u * path + (up ? 1u : 0u);
+      lo = up ? m : lo;
+      hi = up ? hi : m;
+    }
+  }
+  uint32_t ilx = (uint32_t)__builtin_amdgcn_readlane((int)path, 0), ihx = (uint32_t)__builtin_amdgcn_readlane((int)path, 1);
+  uint32_t ily = (uint32_t)__builtin_amdgcn_readlane((int)path, 2), ihy = (uint32_t)__builtin_amdgcn_readlane((int)path, 3);
+  uint32_t ilz = (uint32_t)__builtin_amdgcn_readlane((int)path, 4), ihz = (uint32_t)__builtin_amdgcn_readlane((int)path, 5);
+  while (L > 0 && (ihx - ilx + 1) * (ihy - ily + 1) * (ihz - ilz + 1) > 64) {
+    L--;
+    ilx >>= 1; ihx >>= 1; ily >>= 1; ihy >>= 1; ilz >>= 1; ihz >>= 1;
+  }
+  const uint32_t nx = ihx - ilx + 1, ny = ihy - ily + 1, nz = ihz - ilz + 1;
+  bool put = false;
+  int32_t node = 0;
+  if ((uint32_t)lane < nx * ny * nz) {
+    const uint32_t cx = ilx + (uint32_t)lane % nx, cy = ily + ((uint32_t)lane / nx) % ny,
+                   cz = ilz + (uint32_t)lane / (nx * ny);
+    const uint32_t prefix = spread3(cx) | (spread3(cy) << 1) | (spread3(cz) << 2);
+    const int32_t e = a.cells[(((int64_t)1 << (3 * L)) - 1) / 7 + prefix];
+    if (e >= 0) {
+      node = e >> 5;
+      const int sh = L - (e & 31);
+      const uint32_t fx = ((cx >> sh) << sh) > ilx ? ((cx >> sh) << sh) : ilx;
+      const uint32_t fy = ((cy >> sh) << sh) > ily ? ((cy >> sh) << sh) : ily;
+      const uint32_t fz = ((cz >> sh) << sh) > ilz ? ((cz >> sh) << sh) : ilz;
+      put = cx == fx && cy == fy && cz == fz;
+    }
+  }
+  const unsigned long long pm = __ballot(put);
+  if (put) out[__builtin_amdgcn_mbcnt_hi((uint32_t)(pm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)pm, 0))] = node;
+  return __popcll(pm);
+}
+
 // GL = lanes per scan group. GL = 64: the wave scans every staged point of its box B. GL < 64:
 // the wave's lanes form 64/GL aligned kd sub-buckets (query order), each with its own box
 // B_g (union of its joined lanes' balls, inside B); a lane scans only the staged points of its
@@ -1031,55 +1086,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
     int32_t start = 0;
     int tail = 1;
     if (a.cells) {
-      // Start from the cell tables: the cells of level L (the octree's own midpoint grid) that
-      // B overlaps, one lane each. Per axis, the cell index of a coordinate is the bit path of
-      // its comparisons with the successive midpoints (x > mid goes high, octree.cpp:105-108),
-      // monotone in the coordinate, so B's cells are an index box [il, ih]^3 and every target
-      // point in B lies in one of them; the table gives the node holding all points of a cell
-      // (the depth-L node or the leaf above it; a leaf spanning several cells is queued once,
-      // from its first cell in the box).
-      int L = a.cell_lmax;
-      uint32_t path = 0;
-      if (lane < 6) {
-        const int ax = lane >> 1;
-        const double v = (lane & 1) ? (ax == 0 ? bhx : ax == 1 ? bhy : bhz) : (ax == 0 ? blx : ax == 1 ? bly : blz);
-        double lo = ax == 0 ? a.root_lo[0] : ax == 1 ? a.root_lo[1] : a.root_lo[2];
-        double hi = ax == 0 ? a.root_hi[0] : ax == 1 ? a.root_hi[1] : a.root_hi[2];
-        for (int l = 0; l < L; l++) {
-          const double m = (lo + hi) / 2;
-          const bool up = v > m;
-          path = 2u * path + (up ? 1u : 0u);
-          lo = up ? m : lo;
-          hi = up ? hi : m;
-        }
-      }
-      uint32_t ilx = (uint32_t)__builtin_amdgcn_readlane((int)path, 0), ihx = (uint32_t)__builtin_amdgcn_readlane((int)path, 1);
-      uint32_t ily = (uint32_t)__builtin_amdgcn_readlane((int)path, 2), ihy = (uint32_t)__builtin_amdgcn_readlane((int)path, 3);
-      uint32_t ilz = (uint32_t)__builtin_amdgcn_readlane((int)path, 4), ihz = (uint32_t)__builtin_amdgcn_readlane((int)path, 5);
-      while (L > 0 && (ihx - ilx + 1) * (ihy - ily + 1) * (ihz - ilz + 1) > 64) {
-        L--;
-        ilx >>= 1; ihx >>= 1; ily >>= 1; ihy >>= 1; ilz >>= 1; ihz >>= 1;
-      }
-      const uint32_t nx = ihx - ilx + 1, ny = ihy - ily + 1, nz = ihz - ilz + 1;
-      bool put = false;
-      int32_t node = 0;
-      if ((uint32_t)lane < nx * ny * nz) {
-        const uint32_t cx = ilx + (uint32_t)lane % nx, cy = ily + ((uint32_t)lane / nx) % ny,
-                       cz = ilz + (uint32_t)lane / (nx * ny);
-        const uint32_t prefix = spread3(cx) | (spread3(cy) << 1) | (spread3(cz) << 2);
-        const int32_t e = a.cells[(((int64_t)1 << (3 * L)) - 1) / 7 + prefix];
-        if (e >= 0) {
-          node = e >> 5;
-          const int sh = L - (e & 31);
-          const uint32_t fx = ((cx >> sh) << sh) > ilx ? ((cx >> sh) << sh) : ilx;
-          const uint32_t fy = ((cy >> sh) << sh) > ily ? ((cy >> sh) << sh) : ily;
-          const uint32_t fz = ((cz >> sh) << sh) > ilz ? ((cz >> sh) << sh) : ilz;
-          put = cx == fx && cy == fy && cz == fz;
-        }
-      }
-      const unsigned long long pm = __ballot(put);
-      if (put) queue[__builtin_amdgcn_mbcnt_hi((uint32_t)(pm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)pm, 0))] = node;
-      tail = __popcll(pm);
+      tail = cell_starts(a, blx, bly, blz, bhx, bhy, bhz, lane, queue);
       if (a.dbg && lane == 0) atomicAdd(&a.dbg[21], (unsigned long long)tail);
     } else if (a.lca_descent) {
       while (true) {
@@ -1446,15 +1453,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
 // (best <= u and the window test). Leaves of boxes with s > u (1 + 2^-47) only hold points with
 // fl(d2) > best (1 + 2^-48) (monotone rounding, see k_nn3), so nothing in the window is missed.
 // No usable guess or an overflowing candidate set -> per-lane search (k_nn3_list).
-constexpr int kBallFrontier = 256;
+constexpr int kBallStack = 512;
 constexpr int kBallPoints = 1024;
-constexpr int kBallLdsBytes = 2 * kBallFrontier * 4 + kBallPoints * 4;
+constexpr int kBallLdsBytes = kBallStack * 4 + kBallPoints * 4;
 
 __global__ void __launch_bounds__(64) k_nn_ball(NNLaunch a) {
   extern __shared__ __attribute__((aligned(16))) unsigned long long lds_stack[];
-  int32_t* fr0 = reinterpret_cast<int32_t*>(lds_stack);
-  int32_t* fr1 = fr0 + kBallFrontier;
-  int32_t* plist = fr1 + kBallFrontier;
+  int32_t* stack = reinterpret_cast<int32_t*>(lds_stack);
+  int32_t* plist = stack + kBallStack;
   const int lane = threadIdx.x;
   const unsigned cnt = a.fb_count[1];
   for (unsigned j = blockIdx.x; j < cnt; j += gridDim.x) {
@@ -1466,77 +1472,75 @@ __global__ void __launch_bounds__(64) k_nn_ball(NNLaunch a) {
       continue;
     }
     const double thr = u * (1.0 + kFastPrune);
-    int nf = 1, npts = 0;
+    int tail = 1, npts = 0;
     bool overflow = false;
-    int32_t* cur = fr0;
-    int32_t* nxt = fr1;
     wave_lds_fence();
-    if (lane == 0) cur[0] = 0;
+    if (a.cells) {
+      // every point with fl(d2) <= thr lies in the box q +- r (see k_nn4's radius)
+      const double amax = __builtin_fmax(__builtin_fabs(qx), __builtin_fmax(__builtin_fabs(qy), __builtin_fabs(qz)));
+      const double r = __builtin_sqrt(thr) * (1.0 + 0x1p-40) + amax * 0x1p-45;
+      tail = cell_starts(a, qx - r, qy - r, qz - r, qx + r, qy + r, qz + r, lane, stack);
+    } else if (lane == 0) {
+      stack[0] = 0;
+    }
     wave_lds_fence();
-    while (nf > 0) {
-      int nn = 0;
-      for (int base = 0; base < nf; base += 64) {
-        const int jj = base + lane;
-        const bool has = jj < nf;
-        bool leaf = false;
-        int32_t first = 0;
-        uint32_t meta = 0, kids = 0;
-        if (has) {
-          const NodeRec* rr = a.nodes + cur[jj];
-          const int2 topo = *reinterpret_cast<const int2*>(&rr->first);
-          first = topo.x;
-          meta = (uint32_t)topo.y;
-          leaf = (meta & kLeafBit) != 0;
-          if (!leaf) {
-            const double2 l01 = *reinterpret_cast<const double2*>(&rr->lo[0]);
-            const double2 l2h0 = *reinterpret_cast<const double2*>(&rr->lo[2]);
-            const double2 h12 = *reinterpret_cast<const double2*>(&rr->hi[1]);
-            const double lx = l01.x, ly = l01.y, lz = l2h0.x, hx = l2h0.y, hy = h12.x, hz = h12.y;
-            const double mx = (lx + hx) / 2, my = (ly + hy) / 2, mz = (lz + hz) / 2;
-            const double ax0 = smax(0.0, smax(lx - qx, qx - mx)), ax1 = smax(0.0, smax(mx - qx, qx - hx));
-            const double ay0 = smax(0.0, smax(ly - qy, qy - my)), ay1 = smax(0.0, smax(my - qy, qy - hy));
-            const double az0 = smax(0.0, smax(lz - qz, qz - mz)), az1 = smax(0.0, smax(mz - qz, qz - hz));
-            const double sx[2] = {ax0 * ax0, ax1 * ax1};
-            const double sy[2] = {ay0 * ay0, ay1 * ay1};
-            const double sz[2] = {az0 * az0, az1 * az1};
-            const uint32_t mask = meta & 0xffu;
-#pragma unroll
-            for (int o = 0; o < 8; o++) {
-              const double c = sx[o & 1] + sy[(o >> 1) & 1] + sz[o >> 2];
-              kids |= (((mask >> o) & 1u) && !(c > thr)) ? (1u << o) : 0u;
-            }
-          }
-        }
-        const int lcnt = (has && leaf) ? (int)(meta & ~kLeafBit) : 0;
-        int ltot;
-        const int lincl = wave_incl_scan(lcnt, &ltot);
-        const int lpos = npts + lincl - lcnt;
-        if (lcnt > 0 && lpos + lcnt <= kBallPoints)
-          for (int c = 0; c < lcnt; c++) plist[lpos + c] = first + c;
-        npts += ltot;
-        const int nch = __builtin_popcount(kids);
-        int tot;
-        const int incl = wave_incl_scan(nch, &tot);
-        int off = nn + incl - nch;
-        if (off + nch <= kBallFrontier) {
+    // LIFO batches of up to 64 nodes, sphere test s <= thr on the children
+    while (tail > 0) {
+      const int batch = tail < 64 ? tail : 64;
+      const bool has = lane < batch;
+      bool leaf = false;
+      int32_t first = 0;
+      uint32_t meta = 0, kids = 0;
+      if (has) {
+        const NodeRec* rr = a.nodes + stack[tail - batch + lane];
+        const int2 topo = *reinterpret_cast<const int2*>(&rr->first);
+        first = topo.x;
+        meta = (uint32_t)topo.y;
+        leaf = (meta & kLeafBit) != 0;
+        if (!leaf) {
+          const double2 l01 = *reinterpret_cast<const double2*>(&rr->lo[0]);
+          const double2 l2h0 = *reinterpret_cast<const double2*>(&rr->lo[2]);
+          const double2 h12 = *reinterpret_cast<const double2*>(&rr->hi[1]);
+          const double lx = l01.x, ly = l01.y, lz = l2h0.x, hx = l2h0.y, hy = h12.x, hz = h12.y;
+          const double mx = (lx + hx) / 2, my = (ly + hy) / 2, mz = (lz + hz) / 2;
+          const double ax0 = smax(0.0, smax(lx - qx, qx - mx)), ax1 = smax(0.0, smax(mx - qx, qx - hx));
+          const double ay0 = smax(0.0, smax(ly - qy, qy - my)), ay1 = smax(0.0, smax(my - qy, qy - hy));
+          const double az0 = smax(0.0, smax(lz - qz, qz - mz)), az1 = smax(0.0, smax(mz - qz, qz - hz));
+          const double sx[2] = {ax0 * ax0, ax1 * ax1};
+          const double sy[2] = {ay0 * ay0, ay1 * ay1};
+          const double sz[2] = {az0 * az0, az1 * az1};
           const uint32_t mask = meta & 0xffu;
-          uint32_t kk = kids;
-          while (kk) {
-            const uint32_t o = (uint32_t)__builtin_ctz(kk);
-            kk &= kk - 1u;
-            nxt[off++] = first + __builtin_popcount(mask & ((1u << o) - 1u));
+#pragma unroll
+          for (int o = 0; o < 8; o++) {
+            const double c = sx[o & 1] + sy[(o >> 1) & 1] + sz[o >> 2];
+            kids |= (((mask >> o) & 1u) && !(c > thr)) ? (1u << o) : 0u;
           }
         }
-        nn += tot;
       }
-      if (npts > kBallPoints || nn > kBallFrontier) {
+      const int lcnt = (has && leaf) ? (int)(meta & ~kLeafBit) : 0;
+      int ltot;
+      const int lincl = wave_incl_scan(lcnt, &ltot);
+      const int lpos = npts + lincl - lcnt;
+      if (lcnt > 0 && lpos + lcnt <= kBallPoints)
+        for (int c = 0; c < lcnt; c++) plist[lpos + c] = first + c;
+      npts += ltot;
+      const int nch = __builtin_popcount(kids);
+      int tot;
+      const int incl = wave_incl_scan(nch, &tot);
+      tail -= batch;
+      if (npts > kBallPoints || tail + tot > kBallStack) {
         overflow = true;
         break;
       }
-      int32_t* t = cur;
-      cur = nxt;
-      nxt = t;
-      nf = nn;
+      int off = tail + incl - nch;
+      const uint32_t mask = meta & 0xffu;
+      uint32_t kk = kids;
+      while (kk) {
+        const uint32_t o = (uint32_t)__builtin_ctz(kk);
+        kk &= kk - 1u;
+        stack[off++] = first + __builtin_popcount(mask & ((1u << o) - 1u));
+      }
+      tail += tot;
       wave_lds_fence();
     }
     if (a.dbg && lane == 0) {
