@@ -1237,15 +1237,30 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
         }
         const int m = __popcll(im);
         scanned_pts += m;
-        for (int k = 0; k < m; k++) {
-          const float4 pt = stage32[k];
+        // lockstep over the staged points (16-B broadcast reads, four in flight per step)
+        auto eval = [&](const float4 pt) {
           const float dx = pt.x - qx32, dy = pt.y - qy32, dz = pt.z - qz32;
           const float sq = __builtin_fmaf(dz, dz, __builtin_fmaf(dy, dy, dx * dx));
           const bool lt = sq < s1;
           s2 = __builtin_amdgcn_fmed3f(s1, s2, sq);
           s1 = lt ? sq : s1;
           p1 = lt ? __float_as_int(pt.w) : p1;
+        };
+        typedef int v4i __attribute__((ext_vector_type(4)));
+        const v4i* st4 = reinterpret_cast<const v4i*>(stage32);
+        auto ld = [&](int k) {
+          const v4i v = st4[k];
+          return make_float4(__int_as_float(v.x), __int_as_float(v.y), __int_as_float(v.z), __int_as_float(v.w));
+        };
+        int k = 0;
+        for (; k + 4 <= m; k += 4) {
+          const float4 t0 = ld(k), t1 = ld(k + 1), t2 = ld(k + 2), t3 = ld(k + 3);
+          eval(t0);
+          eval(t1);
+          eval(t2);
+          eval(t3);
         }
+        for (; k < m; k++) eval(ld(k));
       }
       // fp64 distance of the fp32 winner, exactly as the leaf scan computes it (octree.cpp:139-144)
       double b64 = __builtin_inf();
