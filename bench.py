@@ -208,7 +208,8 @@ def main() -> int:
             "data": "synthetic (icp_synth_pair: N(0, diag(5,5,1)^2) target seed 42; source = R^T(target - t) "
                     "+ 1 mm noise, 1% outliers, shuffled, seed 43)",
             "config": {
-                "workload": f"config4: {n}<->{n} synthetic pair, full ICP iteration (engine rules, octree 10/20), "
+                "workload": f"{CONFIG_NAMES.get(n, 'custom')}: {n}<->{n} synthetic pair, full ICP iteration "
+                            f"(engine rules, octree leaf 10 / depth 20), "
                             f"source sharded over {world} GPU(s), target octree replicated",
                 "n_target": n, "n_source": n, "parallelism": f"source-shard x{world} (RCCL all-gather of 2 "
                 "moment records per iteration)",
