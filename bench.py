@@ -36,6 +36,8 @@ sys.path.insert(0, str(ROOT))
 
 METRIC = "M correspondences/sec per ICP iter at 1/2/4/8 GPUs; final RMSE vs CPU ref"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
+# BASELINE.json configs by cloud size (config 3 is the LAS pair: tests/test_gpu_lasflow.py)
+CONFIG_NAMES = {100_000: "config2", 10_000_000: "config4", 50_000_000: "config5"}
 
 
 def shard_range(n: int, rank: int, world: int) -> tuple[int, int]:
