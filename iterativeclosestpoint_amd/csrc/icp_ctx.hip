@@ -113,18 +113,25 @@ int icp_hip_create(icp_hip_ctx** out, int device) {
   if (const char* v = std::getenv("ICP_SCAN32")) c->scan32 = std::atoi(v);
   if (const char* v = std::getenv("ICP_LCA")) c->lca_descent = std::atoi(v);
   if (const char* v = std::getenv("ICP_CELLS")) c->use_cells = std::atoi(v);
+  if (const char* v = std::getenv("ICP_XCD")) c->xcd_remap = std::atoi(v);
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
     delete c;
     return fail(ICP_HIP_EDEVICE, "hipStreamCreate failed");
   }
   for (hipEvent_t* ev : {&c->ev_it0, &c->ev_it1, &c->ev_nn0, &c->ev_nn1}) (void)hipEventCreate(ev);
-  if (dalloc(&c->it, 1) != hipSuccess || hipHostMalloc(reinterpret_cast<void**>(&c->h_it), sizeof(IterDev)) != hipSuccess ||
+  if (dalloc(&c->it, 1) != hipSuccess ||
+      hipHostMalloc(reinterpret_cast<void**>(&c->h_it), sizeof(IterDev), hipHostMallocMapped | hipHostMallocCoherent) !=
+          hipSuccess ||
+      hipHostGetDevicePointer(reinterpret_cast<void**>(&c->h_it_dev), c->h_it, 0) != hipSuccess ||
       dalloc(&c->counters, 2) != hipSuccess || dalloc(&c->Tbuf, 16) != hipSuccess ||
       dalloc(&c->fb_count, 3) != hipSuccess) {
     icp_hip_destroy(c);
     return fail(ICP_HIP_ENOMEM, "context allocation failed");
   }
   (void)hipMemset(c->it, 0, sizeof(IterDev));
+  (void)hipMemset(c->fb_count, 0, 3 * sizeof(unsigned int));
+  std::memset(c->h_it, 0, sizeof(IterDev));
+  c->lists_zero = true;
   *out = c;
   return ICP_HIP_OK;
 }
@@ -300,8 +307,7 @@ int icp_hip_set_source(icp_hip_ctx* c, const double* xyz, int64_t n) {
   HIP_TRY(hipSetDevice(c->device));
   free_source(c);
   c->n_src = n;
-  const int levels = c->levels > 0 ? c->levels : 20;
-  c->nb_nn = nn_num_blocks(n, levels);
+  c->nb_mom = moments_num_parts(n);
   c->nb_cull = cull_num_blocks(n);
   HIP_TRY(dalloc(&c->x, n));
   HIP_TRY(dalloc(&c->y, n));
@@ -311,8 +317,8 @@ int icp_hip_set_source(icp_hip_ctx* c, const double* xyz, int64_t n) {
   HIP_TRY(dalloc(&c->dist, n));
   HIP_TRY(dalloc(&c->fb_list, 3 * (size_t)n));
   HIP_TRY(dalloc(&c->fb_u, (size_t)n));
-  HIP_TRY(dalloc(&c->mparts, (size_t)(c->nb_nn + 2 * ((c->nb_nn + 255) / 256) + 4)));
-  HIP_TRY(dalloc(&c->cparts, (size_t)(c->nb_cull + 2 * ((c->nb_cull + 255) / 256) + 4)));
+  HIP_TRY(dalloc(&c->mparts, (size_t)(c->nb_mom + merge_scratch_entries(c->nb_mom))));
+  HIP_TRY(dalloc(&c->cparts, (size_t)(c->nb_cull + merge_scratch_entries(c->nb_cull))));
   if (n == 0) return ICP_HIP_OK;
   // Spatially compact query order (kd buckets of 64 = one wave), computed on the host.
   std::vector<int32_t> perm;
@@ -355,7 +361,7 @@ int icp_hip_iterate(icp_hip_ctx* c, const double* T_apply, int iter, int rules, 
   a.z = c->z;
   a.pos_out = c->pos;
   a.dist_out = c->dist;
-  a.part = c->mparts;
+  a.part = nullptr;  // moments: launch_moments below
   a.counters = c->counters;
   a.n = c->n_src;
   a.n_nodes = (int32_t)c->n_nodes;
@@ -369,6 +375,7 @@ int icp_hip_iterate(icp_hip_ctx* c, const double* T_apply, int iter, int rules, 
   a.lca_descent = c->lca_descent;
   a.cells = c->cells;
   a.cell_lmax = c->cell_lmax;
+  a.xcd_remap = c->xcd_remap;
   for (int k = 0; k < 3; k++) {
     a.root_lo[k] = c->root_box[k];
     a.root_hi[k] = c->root_box[3 + k];
@@ -382,7 +389,8 @@ int icp_hip_iterate(icp_hip_ctx* c, const double* T_apply, int iter, int rules, 
   a.fb_u2 = c->fb_u;
   a.fb_count = c->fb_count;
   a.have_prev = c->have_prev ? 1 : 0;
-  HIP_TRY(hipMemsetAsync(c->fb_count, 0, 3 * sizeof(unsigned int), s));
+  if (!c->lists_zero) HIP_TRY(hipMemsetAsync(c->fb_count, 0, 3 * sizeof(unsigned int), s));
+  c->lists_zero = false;
   if (std::getenv("ICP_NN_DEBUG")) {
     if (!c->dbg) HIP_TRY(dalloc(&c->dbg, 24));
     HIP_TRY(hipMemsetAsync(c->dbg, 0, 24 * sizeof(unsigned long long), s));
@@ -392,12 +400,15 @@ int icp_hip_iterate(icp_hip_ctx* c, const double* T_apply, int iter, int rules, 
   a.ev_fast_done = c->nn_variant >= 3 ? c->ev_nn1 : nullptr;
   HIP_TRY(launch_nn(a, s));
   if (c->nn_variant < 3) HIP_TRY(hipEventRecord(c->ev_nn1, s));
-  HIP_TRY(launch_merge_moments(c->mparts, c->nb_nn, &c->it->m_local, s));
+  // residual moments -> mean, std, threshold (one rank: fused into the last merge level)
   const bool multi = c->nranks > 1;
-  if (multi)
+  const MomentsFinalize fin{sigma_multiplier, iter, rules == ICP_RULES_ENGINE ? 1 : 0};
+  HIP_TRY(launch_moments(c->dist, c->n_src, c->mparts, s));
+  HIP_TRY(launch_merge_moments(c->mparts, c->nb_mom, c->it, multi ? nullptr : &fin, s));
+  if (multi) {
     RCCL_TRY(ncclAllGather(&c->it->m_local, c->gm, sizeof(Moments) / sizeof(double), ncclDouble, c->comm, s));
-  HIP_TRY(launch_finalize_moments(multi ? c->gm : nullptr, multi ? c->nranks : 1, c->it, sigma_multiplier, iter,
-                                  rules == ICP_RULES_ENGINE ? 1 : 0, s));
+    HIP_TRY(launch_finalize_moments(c->gm, c->nranks, c->it, fin, s));
+  }
   CullLaunch cl;
   cl.x = c->x;
   cl.y = c->y;
@@ -408,15 +419,19 @@ int icp_hip_iterate(icp_hip_ctx* c, const double* T_apply, int iter, int rules, 
   cl.it = c->it;
   cl.part = c->cparts;
   cl.n = c->n_src;
+  cl.xcd_remap = c->xcd_remap;
   HIP_TRY(launch_cull_cov(cl, s));
-  HIP_TRY(launch_merge_cov(c->cparts, c->nb_cull, &c->it->c_local, s));
-  if (multi)
+  // covariance moments -> RMSE; the finished record is stored into pinned host memory
+  const IterPublish pub{c->h_it_dev, c->fb_count};
+  HIP_TRY(launch_merge_cov(c->cparts, c->nb_cull, c->it, multi ? nullptr : &pub, s));
+  if (multi) {
     RCCL_TRY(ncclAllGather(&c->it->c_local, c->gc, sizeof(CovMoments) / sizeof(double), ncclDouble, c->comm, s));
-  HIP_TRY(launch_finalize_cov(multi ? c->gc : nullptr, multi ? c->nranks : 1, c->it, s));
-  HIP_TRY(hipMemcpyAsync(c->h_it, c->it, sizeof(IterDev), hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipMemcpyAsync(c->last_lists, c->fb_count, 3 * sizeof(unsigned int), hipMemcpyDeviceToHost, s));
+    HIP_TRY(launch_finalize_cov(c->gc, c->nranks, c->it, pub, s));
+  }
   HIP_TRY(hipEventRecord(c->ev_it1, s));
   HIP_TRY(hipStreamSynchronize(s));
+  c->lists_zero = true;
+  for (int k = 0; k < 3; k++) c->last_lists[k] = (unsigned int)c->h_it->pad[k];
   const IterDev& h = *c->h_it;
   out->n = (int64_t)h.m_global.n;
   out->mean = h.mean;
@@ -545,6 +560,7 @@ int icp_hip_nn(icp_hip_ctx* c, const double* q, int64_t n, int32_t* idx_out, dou
   a.lca_descent = c->lca_descent;
   a.cells = c->cells;
   a.cell_lmax = c->cell_lmax;
+  a.xcd_remap = c->xcd_remap;
   for (int k = 0; k < 3; k++) {
     a.root_lo[k] = c->root_box[k];
     a.root_hi[k] = c->root_box[3 + k];
@@ -559,6 +575,7 @@ int icp_hip_nn(icp_hip_ctx* c, const double* q, int64_t n, int32_t* idx_out, dou
     a.fb_u2 = fbu;
     a.fb_count = c->fb_count;
     if (e == hipSuccess) e = hipMemsetAsync(c->fb_count, 0, 3 * sizeof(unsigned int), c->stream);
+    c->lists_zero = false;
     if (e == hipSuccess) e = launch_nn(a, c->stream);
     if (e == hipSuccess)
       e = hipMemcpyAsync(c->last_lists, c->fb_count, 3 * sizeof(unsigned int), hipMemcpyDeviceToHost, c->stream);
@@ -603,6 +620,7 @@ int icp_hip_traversal_counts(icp_hip_ctx* c, double* mean_entries, double* mean_
   a.lca_descent = c->lca_descent;
   a.cells = c->cells;
   a.cell_lmax = c->cell_lmax;
+  a.xcd_remap = c->xcd_remap;
   for (int k = 0; k < 3; k++) {
     a.root_lo[k] = c->root_box[k];
     a.root_hi[k] = c->root_box[3 + k];

@@ -16,6 +16,7 @@ struct icp_hip_ctx {
   int scan32 = 1;         // fp32 filter scan in the wave search (ICP_SCAN32=0: fp64 scan)
   int lca_descent = 1;    // uniform descent before the wave's breadth-first walk (ICP_LCA=0: off)
   int use_cells = 1;      // start the wave walk from the cell tables (ICP_CELLS=0: off)
+  int xcd_remap = 0;      // XCD-contiguous block order for search and cull (ICP_XCD=1; measured: no gain)
   hipStream_t stream = nullptr;
   hipEvent_t ev_it0 = nullptr, ev_it1 = nullptr, ev_nn0 = nullptr, ev_nn1 = nullptr;
 
@@ -44,13 +45,15 @@ struct icp_hip_ctx {
   unsigned int last_lists[3] = {0, 0, 0};  // exact / ball / per-lane list sizes of the last search
   icp::Moments* mparts = nullptr;
   icp::CovMoments* cparts = nullptr;
-  int64_t nb_nn = 0, nb_cull = 0;
+  int64_t nb_mom = 0, nb_cull = 0;     // residual-moment parts, cull blocks
+  bool lists_zero = true;               // fb_count is zero (reset by each iteration's publish)
   bool have_results = false;
   bool have_prev = false;  // dist[] holds residuals of the resident queries (search guess)
 
   // per-iteration record
   icp::IterDev* it = nullptr;
-  icp::IterDev* h_it = nullptr;  // pinned
+  icp::IterDev* h_it = nullptr;      // pinned, coherent: the publishing kernel stores into it
+  icp::IterDev* h_it_dev = nullptr;  // its device address
   unsigned long long* counters = nullptr;
   double* Tbuf = nullptr;
 

@@ -10,8 +10,9 @@
 
 namespace icp {
 
-// Device-resident per-iteration record. Written by the finalize kernels, read by the cull
-// kernel (threshold) and copied to the host once per iteration.
+// Per-iteration record. Device-resident copy written by the merge/finalize kernels (the cull
+// kernel reads the threshold from it); the last kernel of the iteration stores the finished
+// record into pinned host memory (IterPublish), the one host read of the iteration.
 struct IterDev {
   Moments m_local;      // this rank's residual moments
   Moments m_global;     // merged over ranks (rank order)
@@ -44,7 +45,7 @@ struct NNLaunch {
   int32_t* fb_list2;       // variant 4: queries a wave did not take -> one-wave ball search
   double* fb_u2;           // variant 4: the distance guess u of each fb_list2 entry
   int32_t* fb_list3;       // variant 4: queries left to the per-lane certified search
-  unsigned int* fb_count;  // [0] exact, [1] ball, [2] per-lane list sizes; zeroed before the launch
+  unsigned int* fb_count;  // [0] exact, [1] ball, [2] per-lane list sizes; zero at the launch
   hipEvent_t ev_fast_done; // optional: recorded right after the fast kernel
   int have_prev;           // variant 4: dist_out holds the previous residuals of these queries
   int scan_group;          // variant 4: lanes per scan group (8, 16, 32 or 64 = whole wave)
@@ -55,6 +56,7 @@ struct NNLaunch {
   int cell_lmax;           // deepest table level
   double root_lo[3], root_hi[3];  // root box (the octree's midpoint recursion starts here)
   unsigned long long* dbg; // optional diagnostics of the wave-cooperative search (ICP_NN_DEBUG)
+  int xcd_remap;           // variant 4: each XCD takes one contiguous range of query blocks
 };
 
 // Threads per block of the NN kernel for a given stack depth.
@@ -62,10 +64,30 @@ int nn_block_threads(int levels);
 int64_t nn_num_blocks(int64_t n, int levels);
 hipError_t launch_nn(const NNLaunch& a, hipStream_t s);
 
-hipError_t launch_merge_moments(const Moments* part, int64_t nparts, Moments* out, hipStream_t s);
-// Merge `nranks` gathered moments (or `local` when gathered == null), compute mean/std/threshold.
-hipError_t launch_finalize_moments(const Moments* gathered, int nranks, IterDev* it, double k_sigma,
-                                   int iter, int engine_rules, hipStream_t s);
+// Residual moments of the settled queries in fixed parts (deterministic), then the merges.
+int64_t moments_num_parts(int64_t n);
+hipError_t launch_moments(const double* dist, int64_t n, Moments* part, hipStream_t s);
+// Partial buffers need merge_scratch_entries(nparts) entries of fold scratch behind the partials.
+int64_t merge_scratch_entries(int64_t nparts);
+
+struct MomentsFinalize {
+  double k_sigma;
+  int iter;
+  int engine_rules;
+};
+// Merge the rank's partials into it->m_local; with fin (single rank) also mean/std/threshold.
+hipError_t launch_merge_moments(const Moments* part, int64_t nparts, IterDev* it, const MomentsFinalize* fin,
+                                hipStream_t s);
+// Merge `nranks` gathered moments in rank order and compute mean/std/threshold.
+hipError_t launch_finalize_moments(const Moments* gathered, int nranks, IterDev* it, MomentsFinalize fin,
+                                   hipStream_t s);
+
+// Where the finished record goes: a device-visible pinned host IterDev (list sizes in pad[0..2]);
+// the three list counters are reset for the next search.
+struct IterPublish {
+  IterDev* host;
+  unsigned int* lists;
+};
 
 struct CullLaunch {
   const double* x;
@@ -77,11 +99,15 @@ struct CullLaunch {
   const IterDev* it;
   CovMoments* part;
   int64_t n;
+  int xcd_remap;  // each XCD takes one contiguous range of blocks (target gathers share its L2)
 };
 int64_t cull_num_blocks(int64_t n);
 hipError_t launch_cull_cov(const CullLaunch& a, hipStream_t s);
-hipError_t launch_merge_cov(const CovMoments* part, int64_t nparts, CovMoments* out, hipStream_t s);
-hipError_t launch_finalize_cov(const CovMoments* gathered, int nranks, IterDev* it, hipStream_t s);
+// Merge the rank's partials into it->c_local; with pub (single rank) also RMSE + publish.
+hipError_t launch_merge_cov(const CovMoments* part, int64_t nparts, IterDev* it, const IterPublish* pub,
+                            hipStream_t s);
+// Merge `nranks` gathered covariance moments in rank order, RMSE, publish.
+hipError_t launch_finalize_cov(const CovMoments* gathered, int nranks, IterDev* it, IterPublish pub, hipStream_t s);
 
 hipError_t launch_apply(const double T[12], double* x, double* y, double* z, int64_t n, hipStream_t s);
 

@@ -725,8 +725,8 @@ __global__ void __launch_bounds__(256) k_nn3(NNLaunch a) {
     }
   }
   wave_append(active && !ok, i, a.fb_count, a.fb_list);
-  // residual moments over the certified queries of this block (complete when the fallback list
-  // is empty; otherwise k_moments_fix recomputes every block from the final residuals)
+  // residual moments over the certified queries of this block (launch_nn passes part = null:
+  // k_moments computes them once every search kernel has written its queries)
   if (!a.part) return;
   __syncthreads();
   double* red = reinterpret_cast<double*>(lds_stack);
@@ -780,56 +780,54 @@ __global__ void __launch_bounds__(256) k_nn_fallback(NNLaunch a) {
   }
 }
 
-// When a list is non-empty, rebuild every part's residual moments from the final residuals: one
-// wave per part of `a.part_size` queries (the search kernel's block), at most 4 per lane, wave
-// shuffles only. Same parts and a fixed order: deterministic whatever the list order.
-__global__ void __launch_bounds__(256) k_moments_fix(NNLaunch a, int part_size, int64_t nparts) {
-  if (a.fb_count[0] == 0 && a.fb_count[1] == 0 && a.fb_count[2] == 0) return;
-  const int lane = threadIdx.x & 63;
-  const int64_t part = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  if (part >= nparts) return;
-  const int64_t b0 = part * part_size;
-  double d[4];
-  int cnt = 0;
-  double s = 0.0;
+// Residual moments of the rank's queries in fixed parts of kMomPart queries, once every search
+// kernel has written its residuals: deterministic whatever order the queries were settled in.
+// Thread t of block p holds queries p kMomPart + t + 256 e (e < kMomPer, coalesced); two register
+// passes (mean, then the centered M2, as icpengine.cpp:235-245 computes them over all queries).
+constexpr int kMomPer = 16;
+constexpr int kMomPart = 256 * kMomPer;
+
+__global__ void __launch_bounds__(256) k_moments(const double* __restrict__ dist, int64_t n, Moments* part) {
+  __shared__ double red[2 * 4];
+  const int64_t b0 = (int64_t)blockIdx.x * kMomPart + threadIdx.x;
+  double d[kMomPer];
+  double s1[2] = {0.0, 0.0};
 #pragma unroll
-  for (int k = 0; k < 4; k++) {
-    const int e = lane + 64 * k;
-    const int64_t i = b0 + e;
-    const bool act = e < part_size && i < a.n;
-    d[k] = act ? a.dist_out[i] : 0.0;
-    cnt += act ? 1 : 0;
-    s += act ? d[k] : 0.0;
+  for (int e = 0; e < kMomPer; e++) {
+    const int64_t i = b0 + 256 * e;
+    const bool act = i < n;
+    d[e] = act ? dist[i] : 0.0;
+    s1[0] += act ? 1.0 : 0.0;
+    s1[1] += act ? d[e] : 0.0;
   }
-  const double nb = wave_sum_d((double)cnt);
-  const double mean = wave_sum_d(s) / nb;
-  double m2 = 0.0, bad = 0.0, mn = 1.7976931348623157e308, mx = 0.0;
+  block_sum<2>(s1, red);
+  const double nb = s1[0];
+  const double mean = s1[1] / nb;
+  double s2[2] = {0.0, 0.0};
+  double mn = 1.7976931348623157e308, mx = 0.0;
 #pragma unroll
-  for (int k = 0; k < 4; k++) {
-    const int e = lane + 64 * k;
-    const bool act = e < part_size && b0 + e < a.n;
-    const double dev = act ? d[k] - mean : 0.0;
-    m2 += dev * dev;
-    const bool fin = act && __builtin_isfinite(d[k]);
-    bad += (act && !fin) ? 1.0 : 0.0;
-    mn = fin && d[k] < mn ? d[k] : mn;
-    mx = fin && d[k] > mx ? d[k] : mx;
+  for (int e = 0; e < kMomPer; e++) {
+    const bool act = b0 + 256 * e < n;
+    const double dev = act ? d[e] - mean : 0.0;
+    s2[0] += dev * dev;
+    const bool fin = act && __builtin_isfinite(d[e]);
+    s2[1] += (act && !fin) ? 1.0 : 0.0;
+    mn = fin && d[e] < mn ? d[e] : mn;
+    mx = fin && d[e] > mx ? d[e] : mx;
   }
-  m2 = wave_sum_d(m2);
-  bad = wave_sum_d(bad);
-  mn = wave_min_d(mn);
-  mx = wave_max_d(mx);
-  if (lane == 0) {
+  block_sum<2>(s2, red);
+  block_minmax(mn, mx, red);
+  if (threadIdx.x == 0) {
     Moments m;
     m.n = nb;
     m.mean = mean;
-    m.m2 = m2;
+    m.m2 = s2[0];
     m.dmin = mn;
     m.dmax = mx;
-    m.nbad = bad;
+    m.nbad = s2[1];
     m.pad0 = 0.0;
     m.pad1 = 0.0;
-    a.part[part] = m;
+    part[blockIdx.x] = m;
   }
 }
 
@@ -846,6 +844,18 @@ __global__ void __launch_bounds__(256) k_moments_fix(NNLaunch a, int part_size, 
 // the scanned ones and the window certificate of k_nn3 applies unchanged. Lanes that do not
 // join (outliers: far from the surface, or a wave whose candidate set overflows LDS) are queued
 // for the per-lane certified search (k_nn3_list); uncertified ones for the exact DFS.
+
+// Workgroups are dispatched round-robin over the 8 XCDs (blockIdx % 8 labels the blocks that share
+// one XCD and its 4 MB L2; cdna_hip_programming.md T1). Renumbered so that each such set takes
+// one contiguous range of the grid: the source is in kd-bucket order, so the blocks resident on
+// one XCD cover one compact region of space and share its L2 for the node and point gathers.
+// Bijective for any grid size (the first nb % 8 sets hold one block more). Speed only.
+__device__ __forceinline__ int64_t xcd_block(int remap) {
+  const uint32_t b = blockIdx.x;
+  if (!remap) return b;
+  const uint32_t nb = gridDim.x, set = b & 7u, q = nb >> 3, r = nb & 7u;
+  return (int64_t)set * q + (set < r ? set : r) + (b >> 3);
+}
 
 constexpr int kWaveQueue = 256;     // node ids in the walk's circular work queue
 constexpr int kMaxGroups = 8;       // lane groups of the scan (GL = 8 lanes at the finest)
@@ -955,7 +965,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
   constexpr int G = 64 / GL;
   extern __shared__ __attribute__((aligned(16))) unsigned long long lds_stack[];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t blk = xcd_block(a.xcd_remap);
+  const int64_t i = blk * blockDim.x + threadIdx.x;
   const bool active = i < a.n;
   unsigned char* wl = reinterpret_cast<unsigned char*>(lds_stack) + wv * wave_lds_bytes(GL, PL);
   int32_t* queue = reinterpret_cast<int32_t*>(wl);
@@ -1207,7 +1218,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
                              dmax_(bhz - ocz, ocz - blz)) * (1.0 + 0x1p-40);
     if (ext >= 0x1p-40 && ext <= 0x1p60) {
       const float qx32 = (float)(qx - ocx), qy32 = (float)(qy - ocy), qz32 = (float)(qz - ocz);
-      float4* stage32 = reinterpret_cast<float4*>(wl);
+      // staging area: points in pairs, [x0 x1 y0 y1 z0 z1 w0 w1] (32 B), so that one packed fp32
+      // instruction (v_pk_add/mul/fma_f32) evaluates an axis of two points
+      float* stage32 = reinterpret_cast<float*>(wl);
       float s1 = __builtin_inff(), s2 = __builtin_inff();
       int32_t p1 = -1;
       wave_lds_fence();
@@ -1223,10 +1236,25 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
                          nxtp.z >= blz && nxtp.z <= bhz;
         const unsigned long long im = __ballot(nin);
         const int slot = __builtin_amdgcn_mbcnt_hi((uint32_t)(im >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)im, 0));
-        const float4 v = make_float4((float)(nxtp.x - ocx), (float)(nxtp.y - ocy), (float)(nxtp.z - ocz),
-                                     __int_as_float((int)__double_as_longlong(nxtp.w)));
+        const float vx = (float)(nxtp.x - ocx), vy = (float)(nxtp.y - ocy), vz = (float)(nxtp.z - ocz);
+        const float vw = __int_as_float((int)__double_as_longlong(nxtp.w));
+        const int m = __popcll(im);
         wave_lds_fence();  // previous chunk's reads are done before overwriting the staging slots
-        if (nin) stage32[slot] = v;
+        if (nin) {
+          float* sp = stage32 + 8 * (slot >> 1) + (slot & 1);
+          sp[0] = vx;
+          sp[2] = vy;
+          sp[4] = vz;
+          sp[6] = vw;
+        }
+        if ((m & 1) && lane == 63) {
+          // odd count: the last pair's second point at +inf (its sq = +inf never replaces s1 and
+          // leaves s2 unchanged; no NaN can arise from inf - finite)
+          float* sp = stage32 + 8 * (m >> 1) + 1;
+          sp[0] = __builtin_inff();
+          sp[2] = __builtin_inff();
+          sp[4] = __builtin_inff();
+        }
         wave_lds_fence();
         const int nb = base + 64;
         if (nb + lane < npts) {
@@ -1235,32 +1263,36 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
           const double2 xy = *reinterpret_cast<const double2*>(&p->x);
           nxtp = make_double4(xy.x, xy.y, p->z, __longlong_as_double((long long)g));
         }
-        const int m = __popcll(im);
         scanned_pts += m;
-        // lockstep over the staged points (16-B broadcast reads, four in flight per step)
-        auto eval = [&](const float4 pt) {
-          const float dx = pt.x - qx32, dy = pt.y - qy32, dz = pt.z - qz32;
-          const float sq = __builtin_fmaf(dz, dz, __builtin_fmaf(dy, dy, dx * dx));
+        // lockstep over the staged pairs (16-B broadcast reads). Point 2k is selected before point
+        // 2k + 1: the same sequence of updates as a one-point-at-a-time scan.
+        typedef float f2 __attribute__((ext_vector_type(2)));
+        typedef int v4i __attribute__((ext_vector_type(4)));
+        const f2 qx2 = {qx32, qx32}, qy2 = {qy32, qy32}, qz2 = {qz32, qz32};
+        auto sel = [&](float sq, int w) {
           const bool lt = sq < s1;
           s2 = __builtin_amdgcn_fmed3f(s1, s2, sq);
           s1 = lt ? sq : s1;
-          p1 = lt ? __float_as_int(pt.w) : p1;
+          p1 = lt ? w : p1;
         };
-        typedef int v4i __attribute__((ext_vector_type(4)));
+        auto eval2 = [&](const v4i xy, const v4i zw) {
+          const f2 X = {__int_as_float(xy.x), __int_as_float(xy.y)};
+          const f2 Y = {__int_as_float(xy.z), __int_as_float(xy.w)};
+          const f2 Z = {__int_as_float(zw.x), __int_as_float(zw.y)};
+          const f2 dx = X - qx2, dy = Y - qy2, dz = Z - qz2;
+          const f2 sq = __builtin_elementwise_fma(dz, dz, __builtin_elementwise_fma(dy, dy, dx * dx));
+          sel(sq.x, zw.z);
+          sel(sq.y, zw.w);
+        };
         const v4i* st4 = reinterpret_cast<const v4i*>(stage32);
-        auto ld = [&](int k) {
-          const v4i v = st4[k];
-          return make_float4(__int_as_float(v.x), __int_as_float(v.y), __int_as_float(v.z), __int_as_float(v.w));
-        };
+        const int mp = (m + 1) >> 1;
         int k = 0;
-        for (; k + 4 <= m; k += 4) {
-          const float4 t0 = ld(k), t1 = ld(k + 1), t2 = ld(k + 2), t3 = ld(k + 3);
-          eval(t0);
-          eval(t1);
-          eval(t2);
-          eval(t3);
+        for (; k + 2 <= mp; k += 2) {
+          const v4i a0 = st4[2 * k], b0 = st4[2 * k + 1], a1 = st4[2 * k + 2], b1 = st4[2 * k + 3];
+          eval2(a0, b0);
+          eval2(a1, b1);
         }
-        for (; k < m; k++) eval(ld(k));
+        if (k < mp) eval2(st4[2 * k], st4[2 * k + 1]);
       }
       // fp64 distance of the fp32 winner, exactly as the leaf scan computes it (octree.cpp:139-144)
       double b64 = __builtin_inf();
@@ -1433,32 +1465,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
     atomicAdd(&a.dbg[18], t_p4 - t_p3);
     atomicAdd(&a.dbg[19], t_p5 - t_p4);
   }
-  if (!a.part) return;
-  __syncthreads();
-  double* red = reinterpret_cast<double*>(lds_stack);
-  const bool use = active && written;
-  double s1[2] = {use ? 1.0 : 0.0, use ? d : 0.0};
-  block_sum<2>(s1, red);
-  const double nb = s1[0];
-  const double mean = nb > 0.0 ? s1[1] / nb : 0.0;
-  const double dev = use ? (d - mean) : 0.0;
-  const bool fin = use && __builtin_isfinite(d);
-  double s2[2] = {dev * dev, (use && !fin) ? 1.0 : 0.0};
-  block_sum<2>(s2, red);
-  double mn = fin ? d : 1.7976931348623157e308, mxv = fin ? d : 0.0;
-  block_minmax(mn, mxv, red);
-  if (threadIdx.x == 0) {
-    Moments m;
-    m.n = nb;
-    m.mean = mean;
-    m.m2 = s2[0];
-    m.dmin = mn;
-    m.dmax = mxv;
-    m.nbad = s2[1];
-    m.pad0 = 0.0;
-    m.pad1 = 0.0;
-    a.part[blockIdx.x] = m;
-  }
+  // residual moments: k_moments, once every search kernel has written its queries
 }
 
 // One wave per query for the queries a k_nn4 wave did not take (outliers far from the surface,
@@ -1643,19 +1650,33 @@ __global__ void __launch_bounds__(256) k_nn3_list(NNLaunch a) {
   }
 }
 
-// Fixed-shape tree merge: block b merges parts [256 b, 256 b + 256) pairwise in LDS.
+// Fixed-shape merges of block partials (Chan et al. pairwise formulas), deterministic: the same
+// n always gives the same merge tree. Inner levels: block b merges items [256 b, 256 b + 256),
+// one per thread, pairwise in LDS. Last level: one block, up to 1024 items, thread t merges items
+// 4t..4t+3 as ((0, 1), (2, 3)), then the block's pairwise tree. Every load is independent: no
+// dependent chain longer than log2 of the items.
+constexpr int kLastSpan = 1024;
+
 template <typename T, T (*Merge)(const T&, const T&), T (*Identity)()>
-__global__ void __launch_bounds__(256) k_tree_merge(const T* in, int64_t n, T* out) {
-  __shared__ T sm[256];
+__device__ __forceinline__ T block_tree(T v, T* sm) {
   const int t = threadIdx.x;
-  const int64_t g = (int64_t)blockIdx.x * 256 + t;
-  sm[t] = (g < n) ? in[g] : Identity();
+  sm[t] = v;
   __syncthreads();
   for (int s = 1; s < 256; s <<= 1) {
     if ((t & (2 * s - 1)) == 0) sm[t] = Merge(sm[t], sm[t + s]);
     __syncthreads();
   }
-  if (t == 0) out[blockIdx.x] = sm[0];
+  return sm[0];
+}
+
+template <typename T, T (*Merge)(const T&, const T&), T (*Identity)()>
+__device__ __forceinline__ T block_tree_last(const T* in, int64_t n, T* sm) {
+  const int64_t g = 4 * (int64_t)threadIdx.x;
+  const T i0 = g < n ? in[g] : Identity();
+  const T i1 = g + 1 < n ? in[g + 1] : Identity();
+  const T i2 = g + 2 < n ? in[g + 2] : Identity();
+  const T i3 = g + 3 < n ? in[g + 3] : Identity();
+  return block_tree<T, Merge, Identity>(Merge(Merge(i0, i1), Merge(i2, i3)), sm);
 }
 
 __device__ Moments d_moments_merge(const Moments& a, const Moments& b) { return moments_merge(a, b); }
@@ -1663,18 +1684,85 @@ __device__ Moments d_moments_identity() { return moments_identity(); }
 __device__ CovMoments d_cov_merge(const CovMoments& a, const CovMoments& b) { return cov_merge(a, b); }
 __device__ CovMoments d_cov_identity() { return cov_identity(); }
 
-__global__ void k_finalize_moments(const Moments* gathered, int nranks, IterDev* it, double k_sigma,
-                                   int iter, int engine_rules) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  Moments g = gathered ? gathered[0] : it->m_local;
-  for (int r = 1; r < nranks; r++) g = moments_merge(g, gathered[r]);
+template <typename T, T (*Merge)(const T&, const T&), T (*Identity)()>
+__global__ void __launch_bounds__(256) k_tree_merge(const T* in, int64_t n, T* out) {
+  __shared__ T sm[256];
+  const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const T r = block_tree<T, Merge, Identity>(g < n ? in[g] : Identity(), sm);
+  if (threadIdx.x == 0) out[blockIdx.x] = r;
+}
+
+// mean = sum/row; std = sqrt(variance/row) (icpengine.cpp:235-245); threshold rule of the caller
+__device__ void finalize_moments(IterDev* it, const Moments& g, const MomentsFinalize& f) {
   it->m_global = g;
-  // mean = sum/row; std = sqrt(variance/row) (icpengine.cpp:235-245)
   const double mean = g.mean;
   const double sd = __builtin_sqrt(g.m2 / g.n);
   it->mean = mean;
   it->sd = sd;
-  it->thr = cull_threshold(mean, sd, k_sigma, iter, engine_rules);
+  it->thr = cull_threshold(mean, sd, f.k_sigma, f.iter, f.engine_rules);
+}
+
+// Last level of the rank's moments merge: it->m_local; with fin (one rank) also the statistics.
+__global__ void __launch_bounds__(256) k_merge_moments_last(const Moments* in, int64_t n, IterDev* it,
+                                                           MomentsFinalize fin, int finalize) {
+  __shared__ Moments sm[256];
+  const Moments r = block_tree_last<Moments, d_moments_merge, d_moments_identity>(in, n, sm);
+  if (threadIdx.x == 0) {
+    it->m_local = r;
+    if (finalize) finalize_moments(it, r, fin);
+  }
+}
+
+__global__ void k_finalize_moments(const Moments* gathered, int nranks, IterDev* it, MomentsFinalize fin) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  Moments g = gathered[0];
+  for (int r = 1; r < nranks; r++) g = moments_merge(g, gathered[r]);  // rank order: same bits everywhere
+  finalize_moments(it, g, fin);
+}
+
+// The iteration's record goes straight into the caller's pinned host buffer (no copy engine or
+// blit launch on the critical path): thread 0 completes it in LDS, the block stores it, and the
+// stream synchronisation that follows makes it visible. The list sizes ride along (pad[0..2])
+// and are reset for the next search.
+__device__ void finalize_cov_publish(IterDev* it, const CovMoments& g, IterPublish pub, IterDev* rec) {
+  if (threadIdx.x == 0) {
+    *rec = *it;
+    rec->c_global = g;
+    rec->rmse = (g.n > 0) ? __builtin_sqrt(g.sum_d2 / g.n) : 0.0;  // icpengine.cpp:274-278
+    for (int k = 0; k < 3; k++) {
+      rec->pad[k] = (double)pub.lists[k];
+      pub.lists[k] = 0u;
+    }
+    rec->pad[3] = 0.0;
+    it->c_global = rec->c_global;
+    it->rmse = rec->rmse;
+  }
+  __syncthreads();
+  const double* src = reinterpret_cast<const double*>(rec);
+  double* dst = reinterpret_cast<double*>(pub.host);
+  for (int k = threadIdx.x; k < (int)(sizeof(IterDev) / sizeof(double)); k += blockDim.x) dst[k] = src[k];
+  __threadfence_system();
+}
+
+__global__ void __launch_bounds__(256) k_merge_cov_last(const CovMoments* in, int64_t n, IterDev* it, IterPublish pub,
+                                                       int finalize) {
+  __shared__ CovMoments sm[256];
+  __shared__ IterDev rec;
+  const CovMoments r = block_tree_last<CovMoments, d_cov_merge, d_cov_identity>(in, n, sm);
+  if (!finalize) {
+    if (threadIdx.x == 0) it->c_local = r;
+    return;
+  }
+  if (threadIdx.x == 0) it->c_local = r;
+  finalize_cov_publish(it, r, pub, &rec);
+}
+
+__global__ void __launch_bounds__(64) k_finalize_cov(const CovMoments* gathered, int nranks, IterDev* it,
+                                                     IterPublish pub) {
+  __shared__ IterDev rec;
+  CovMoments g = gathered[0];
+  for (int r = 1; r < nranks; r++) g = cov_merge(g, gathered[r]);  // rank order
+  finalize_cov_publish(it, g, pub, &rec);
 }
 
 constexpr int kCullPer = 4;  // queries per thread of k_cull_cov
@@ -1682,7 +1770,8 @@ constexpr int kCullPer = 4;  // queries per thread of k_cull_cov
 __global__ void __launch_bounds__(256) k_cull_cov(CullLaunch a) {
   __shared__ double red[4 * 9];
   const double thr = a.it->thr;
-  const int64_t base = (int64_t)blockIdx.x * (256 * kCullPer) + threadIdx.x;
+  const int64_t blk = xcd_block(a.xcd_remap);
+  const int64_t base = blk * (256 * kCullPer) + threadIdx.x;
   bool valid[kCullPer];
   double d[kCullPer], ax[kCullPer], ay[kCullPer], az[kCullPer], bx[kCullPer], by[kCullPer], bz[kCullPer];
 #pragma unroll
@@ -1720,7 +1809,7 @@ __global__ void __launch_bounds__(256) k_cull_cov(CullLaunch a) {
   block_sum<8>(s1, red);
   const double nb = s1[0];
   if (nb == 0.0) {
-    if (threadIdx.x == 0) a.part[blockIdx.x] = cov_identity();
+    if (threadIdx.x == 0) a.part[blk] = cov_identity();
     return;
   }
   const double ma[3] = {s1[2] / nb, s1[3] / nb, s1[4] / nb};
@@ -1750,17 +1839,8 @@ __global__ void __launch_bounds__(256) k_cull_cov(CullLaunch a) {
     m.pad[0] = 0.0;
     m.pad[1] = 0.0;
     m.pad[2] = 0.0;
-    a.part[blockIdx.x] = m;
+    a.part[blk] = m;
   }
-}
-
-__global__ void k_finalize_cov(const CovMoments* gathered, int nranks, IterDev* it) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  CovMoments g = gathered ? gathered[0] : it->c_local;
-  for (int r = 1; r < nranks; r++) g = cov_merge(g, gathered[r]);
-  it->c_global = g;
-  // rmse over valid pairs (icpengine.cpp:274-278)
-  it->rmse = (g.n > 0) ? __builtin_sqrt(g.sum_d2 / g.n) : 0.0;
 }
 
 __global__ void k_apply(const double* __restrict__ Tm, double* x, double* y, double* z, int64_t n) {
@@ -1873,15 +1953,19 @@ int64_t nn_num_blocks(int64_t n, int levels) {
   return (n + bs - 1) / bs;
 }
 
-hipError_t launch_nn(const NNLaunch& a, hipStream_t s) {
-  if (a.n <= 0) return hipSuccess;
+// The search kernels only settle queries (pos, residual); the caller computes the residual
+// moments afterwards (launch_moments), so a.part is ignored here.
+hipError_t launch_nn(const NNLaunch& a_in, hipStream_t s) {
+  if (a_in.n <= 0) return hipSuccess;
+  NNLaunch a = a_in;
+  a.part = nullptr;
   const int levels = a.levels < 1 ? 1 : a.levels;
   const int bs = nn_block_threads(levels);
   size_t shmem = (size_t)levels * bs * sizeof(unsigned long long);
   if (shmem < 1024) shmem = 1024;  // also hosts the block reductions
   const unsigned grid = grid_for(a.n, bs);
   if (a.variant == 4 && !a.count) {
-    // wave-cooperative search -> per-lane search for the rest -> exact fallback -> moments repair
+    // wave-cooperative search -> ball search -> per-lane search -> exact fallback
     const int gl = (a.scan_group == 8 || a.scan_group == 16 || a.scan_group == 32) ? a.scan_group : 64;
     const int pl = (gl == 64 && (a.wave_points == 512 || a.wave_points == 768)) ? a.wave_points : 1024;
     const size_t shm4 = (size_t)(bs / kWave) * wave_lds_bytes(gl, pl);
@@ -1898,27 +1982,24 @@ hipError_t launch_nn(const NNLaunch& a, hipStream_t s) {
     else ICP_NN4(64, 1024);
 #undef ICP_NN4
     if (a.ev_fast_done) (void)hipEventRecord(a.ev_fast_done, s);
-    // the lists are short: 64-thread blocks spread them over every CU (latency-bound walks)
-    const unsigned lgrid = (unsigned)((a.n + 63) / 64 < 4096 ? (a.n + 63) / 64 : 4096);
+    // the lists are short (usually empty after the first iteration): small grids of 64-thread
+    // blocks, grid-stride over the list
+    const unsigned lgrid = (unsigned)((a.n + 63) / 64 < 1024 ? (a.n + 63) / 64 : 1024);
     const size_t lshm = (size_t)levels * 64 * sizeof(unsigned long long) < 1024 ? 1024
                         : (size_t)levels * 64 * sizeof(unsigned long long);
     const unsigned bgrid = (unsigned)((a.n < 16384) ? a.n : 16384);
     hipLaunchKernelGGL(k_nn_ball, dim3(bgrid), dim3(64), kBallLdsBytes, s, a);
     hipLaunchKernelGGL(k_nn3_list, dim3(lgrid), dim3(64), lshm, s, a);
     hipLaunchKernelGGL(k_nn_fallback, dim3(lgrid), dim3(64), lshm, s, a);
-    if (a.part) hipLaunchKernelGGL(k_moments_fix, dim3((unsigned)((grid + 3) / 4)), dim3(256), 0, s, a, bs,
-                                   (int64_t)grid);
     return hipGetLastError();
   }
   if (a.variant == 3 && !a.count) {
-    // certified fast path -> exact fallback for the uncertified rest -> moments repair
+    // certified fast path -> exact fallback for the uncertified rest
     if (a.apply) hipLaunchKernelGGL((k_nn3<true>), dim3(grid), dim3(bs), shmem, s, a);
     else hipLaunchKernelGGL((k_nn3<false>), dim3(grid), dim3(bs), shmem, s, a);
     if (a.ev_fast_done) (void)hipEventRecord(a.ev_fast_done, s);
     const unsigned fb_grid = grid < 1024u ? grid : 1024u;
     hipLaunchKernelGGL(k_nn_fallback, dim3(fb_grid), dim3(bs), shmem, s, a);
-    if (a.part) hipLaunchKernelGGL(k_moments_fix, dim3((unsigned)((grid + 3) / 4)), dim3(256), 0, s, a, bs,
-                                   (int64_t)grid);
     return hipGetLastError();
   }
   if (a.variant == 1 || a.count) {
@@ -1941,61 +2022,57 @@ hipError_t launch_nn(const NNLaunch& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-static hipError_t tree_merge_moments(const Moments* in, int64_t n, Moments* scratch, Moments* out,
-                                     hipStream_t s) {
-  // in -> scratch (ceil(n/256)) -> ... -> out (1)
-  const Moments* cur = in;
-  int64_t cn = n;
-  Moments* bufs[2] = {scratch, scratch + ((n + 255) / 256)};
-  int k = 0;
-  while (cn > 256) {
+// Partial buffers hold the block partials followed by the merge scratch (merge_scratch_entries).
+int64_t merge_scratch_entries(int64_t nparts) {
+  int64_t total = 0;
+  for (int64_t cn = nparts; cn > kLastSpan; cn = (cn + 255) / 256) total += (cn + 255) / 256;
+  return total + 1;
+}
+
+template <typename T, T (*Merge)(const T&, const T&), T (*Identity)()>
+static const T* merge_to_last_span(const T* part, int64_t* nparts, hipStream_t s) {
+  // part -> scratch levels (right behind the partials) until the last block's span is left
+  const T* cur = part;
+  T* next = const_cast<T*>(part) + *nparts;
+  int64_t cn = *nparts;
+  while (cn > kLastSpan) {
     const int64_t nb = (cn + 255) / 256;
-    hipLaunchKernelGGL((k_tree_merge<Moments, d_moments_merge, d_moments_identity>), dim3((unsigned)nb),
-                       dim3(256), 0, s, cur, cn, bufs[k]);
-    cur = bufs[k];
+    hipLaunchKernelGGL((k_tree_merge<T, Merge, Identity>), dim3((unsigned)nb), dim3(256), 0, s, cur, cn, next);
+    cur = next;
+    next += nb;
     cn = nb;
-    k ^= 1;
   }
-  hipLaunchKernelGGL((k_tree_merge<Moments, d_moments_merge, d_moments_identity>), dim3(1), dim3(256), 0, s,
-                     cur, cn, out);
+  *nparts = cn;
+  return cur;
+}
+
+hipError_t launch_merge_moments(const Moments* part, int64_t nparts, IterDev* it, const MomentsFinalize* fin,
+                                hipStream_t s) {
+  const Moments* cur = merge_to_last_span<Moments, d_moments_merge, d_moments_identity>(part, &nparts, s);
+  hipLaunchKernelGGL(k_merge_moments_last, dim3(1), dim3(256), 0, s, cur, nparts, it,
+                     fin ? *fin : MomentsFinalize{0.0, 0, 0}, fin ? 1 : 0);
   return hipGetLastError();
 }
 
-static hipError_t tree_merge_cov(const CovMoments* in, int64_t n, CovMoments* scratch, CovMoments* out,
-                                 hipStream_t s) {
-  const CovMoments* cur = in;
-  int64_t cn = n;
-  CovMoments* bufs[2] = {scratch, scratch + ((n + 255) / 256)};
-  int k = 0;
-  while (cn > 256) {
-    const int64_t nb = (cn + 255) / 256;
-    hipLaunchKernelGGL((k_tree_merge<CovMoments, d_cov_merge, d_cov_identity>), dim3((unsigned)nb), dim3(256),
-                       0, s, cur, cn, bufs[k]);
-    cur = bufs[k];
-    cn = nb;
-    k ^= 1;
-  }
-  hipLaunchKernelGGL((k_tree_merge<CovMoments, d_cov_merge, d_cov_identity>), dim3(1), dim3(256), 0, s, cur,
-                     cn, out);
+hipError_t launch_merge_cov(const CovMoments* part, int64_t nparts, IterDev* it, const IterPublish* pub,
+                            hipStream_t s) {
+  const CovMoments* cur = merge_to_last_span<CovMoments, d_cov_merge, d_cov_identity>(part, &nparts, s);
+  hipLaunchKernelGGL(k_merge_cov_last, dim3(1), dim3(256), 0, s, cur, nparts, it,
+                     pub ? *pub : IterPublish{nullptr, nullptr}, pub ? 1 : 0);
   return hipGetLastError();
 }
 
-// The partial buffers are allocated with room for the merge scratch right behind the
-// block partials: parts[0 .. nparts) then 2 * ceil(nparts / 256) + 2 scratch entries.
-hipError_t launch_merge_moments(const Moments* part, int64_t nparts, Moments* out, hipStream_t s) {
-  Moments* scratch = const_cast<Moments*>(part) + nparts;
-  return tree_merge_moments(part, nparts, scratch, out, s);
+hipError_t launch_finalize_moments(const Moments* gathered, int nranks, IterDev* it, MomentsFinalize fin,
+                                   hipStream_t s) {
+  hipLaunchKernelGGL(k_finalize_moments, dim3(1), dim3(64), 0, s, gathered, nranks, it, fin);
+  return hipGetLastError();
 }
 
-hipError_t launch_merge_cov(const CovMoments* part, int64_t nparts, CovMoments* out, hipStream_t s) {
-  CovMoments* scratch = const_cast<CovMoments*>(part) + nparts;
-  return tree_merge_cov(part, nparts, scratch, out, s);
-}
+int64_t moments_num_parts(int64_t n) { return (n + kMomPart - 1) / kMomPart; }
 
-hipError_t launch_finalize_moments(const Moments* gathered, int nranks, IterDev* it, double k_sigma, int iter,
-                                   int engine_rules, hipStream_t s) {
-  hipLaunchKernelGGL(k_finalize_moments, dim3(1), dim3(64), 0, s, gathered, nranks, it, k_sigma, iter,
-                     engine_rules);
+hipError_t launch_moments(const double* dist, int64_t n, Moments* part, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_moments, dim3((unsigned)moments_num_parts(n)), dim3(256), 0, s, dist, n, part);
   return hipGetLastError();
 }
 
@@ -2007,8 +2084,9 @@ hipError_t launch_cull_cov(const CullLaunch& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t launch_finalize_cov(const CovMoments* gathered, int nranks, IterDev* it, hipStream_t s) {
-  hipLaunchKernelGGL(k_finalize_cov, dim3(1), dim3(64), 0, s, gathered, nranks, it);
+hipError_t launch_finalize_cov(const CovMoments* gathered, int nranks, IterDev* it, IterPublish pub,
+                              hipStream_t s) {
+  hipLaunchKernelGGL(k_finalize_cov, dim3(1), dim3(64), 0, s, gathered, nranks, it, pub);
   return hipGetLastError();
 }
 
