@@ -132,6 +132,9 @@ int icp_hip_target_info(icp_hip_ctx* ctx, int64_t* n_nodes, int64_t* n_leaves, i
  * whole device part of the last iterate. */
 int icp_hip_last_timing(icp_hip_ctx* ctx, double* nn_kernel_ms, double* iterate_device_ms);
 
+/* The same for each of the last k iterates (k <= 64), oldest first. Waits for them to finish. */
+int icp_hip_timings(icp_hip_ctx* ctx, int k, double* nn_kernel_ms, double* iterate_device_ms);
+
 int icp_hip_synchronize(icp_hip_ctx* ctx);
 
 const char* icp_hip_last_error(void);

@@ -122,6 +122,7 @@ SIGNATURES = {
     "icp_hip_traversal_counts": (C.c_int, [_P, _D, _D]),
     "icp_hip_target_info": (C.c_int, [_P, C.POINTER(C.c_int64), C.POINTER(C.c_int64), _I32, _I32]),
     "icp_hip_last_timing": (C.c_int, [_P, _D, _D]),
+    "icp_hip_timings": (C.c_int, [_P, C.c_int, _P, _P]),
     "icp_hip_target_build_info": (C.c_int, [_P, _I32, _D]),
     "icp_hip_copy_target": (C.c_int, [_P, _P, _P, _P, _P, _P, _P]),
     "icp_hip_synchronize": (C.c_int, [_P]),
@@ -332,6 +333,12 @@ class Context:
         a, b = C.c_double(), C.c_double()
         _check(lib().icp_hip_last_timing(self._h, C.byref(a), C.byref(b)))
         return a.value, b.value
+
+    def timings(self, k: int):
+        """(search kernel ms, iterate device ms) of each of the last k iterates, oldest first."""
+        a, b = np.zeros(k), np.zeros(k)
+        _check(lib().icp_hip_timings(self._h, k, _ptr(a), _ptr(b)))
+        return a, b
 
     def synchronize(self):
         _check(lib().icp_hip_synchronize(self._h))

@@ -114,11 +114,14 @@ int icp_hip_create(icp_hip_ctx** out, int device) {
   if (const char* v = std::getenv("ICP_LCA")) c->lca_descent = std::atoi(v);
   if (const char* v = std::getenv("ICP_CELLS")) c->use_cells = std::atoi(v);
   if (const char* v = std::getenv("ICP_XCD")) c->xcd_remap = std::atoi(v);
+  if (const char* v = std::getenv("ICP_BALL_GROUPS")) c->ball_groups = std::atoi(v);
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
     delete c;
     return fail(ICP_HIP_EDEVICE, "hipStreamCreate failed");
   }
-  for (hipEvent_t* ev : {&c->ev_it0, &c->ev_it1, &c->ev_nn0, &c->ev_nn1}) (void)hipEventCreate(ev);
+  for (hipEvent_t* ev : {&c->ev_it0, &c->ev_it1}) (void)hipEventCreate(ev);
+  for (auto& r : c->ring)
+    for (hipEvent_t& ev : r) (void)hipEventCreate(&ev);
   if (dalloc(&c->it, 1) != hipSuccess ||
       hipHostMalloc(reinterpret_cast<void**>(&c->h_it), sizeof(IterDev), hipHostMallocMapped | hipHostMallocCoherent) !=
           hipSuccess ||
@@ -151,8 +154,11 @@ void icp_hip_destroy(icp_hip_ctx* c) {
   dfree(c->gc);
   if (c->h_it) (void)hipHostFree(c->h_it);
   if (c->comm) (void)ncclCommDestroy(c->comm);
-  for (hipEvent_t ev : {c->ev_it0, c->ev_it1, c->ev_nn0, c->ev_nn1})
+  for (hipEvent_t ev : {c->ev_it0, c->ev_it1})
     if (ev) (void)hipEventDestroy(ev);
+  for (auto& r : c->ring)
+    for (hipEvent_t ev : r)
+      if (ev) (void)hipEventDestroy(ev);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -351,7 +357,8 @@ int icp_hip_iterate(icp_hip_ctx* c, const double* T_apply, int iter, int rules, 
   if (c->nranks > 1 && !c->comm) return fail(ICP_HIP_ENOTREADY, "communicator not initialised");
   HIP_TRY(hipSetDevice(c->device));
   hipStream_t s = c->stream;
-  HIP_TRY(hipEventRecord(c->ev_it0, s));
+  hipEvent_t* ev = c->ring[c->n_iterates % icp_hip_ctx::kTimingRing];
+  HIP_TRY(hipEventRecord(ev[0], s));
   NNLaunch a;
   std::memset(&a, 0, sizeof(a));
   a.nodes = c->nodes;
@@ -376,6 +383,7 @@ int icp_hip_iterate(icp_hip_ctx* c, const double* T_apply, int iter, int rules, 
   a.cells = c->cells;
   a.cell_lmax = c->cell_lmax;
   a.xcd_remap = c->xcd_remap;
+  a.ball_groups = c->ball_groups;
   for (int k = 0; k < 3; k++) {
     a.root_lo[k] = c->root_box[k];
     a.root_hi[k] = c->root_box[3 + k];
@@ -396,10 +404,10 @@ int icp_hip_iterate(icp_hip_ctx* c, const double* T_apply, int iter, int rules, 
     HIP_TRY(hipMemsetAsync(c->dbg, 0, 24 * sizeof(unsigned long long), s));
     a.dbg = c->dbg;
   }
-  HIP_TRY(hipEventRecord(c->ev_nn0, s));
-  a.ev_fast_done = c->nn_variant >= 3 ? c->ev_nn1 : nullptr;
+  HIP_TRY(hipEventRecord(ev[1], s));
+  a.ev_fast_done = c->nn_variant >= 3 ? ev[2] : nullptr;
   HIP_TRY(launch_nn(a, s));
-  if (c->nn_variant < 3) HIP_TRY(hipEventRecord(c->ev_nn1, s));
+  if (c->nn_variant < 3) HIP_TRY(hipEventRecord(ev[2], s));
   // residual moments -> mean, std, threshold (one rank: fused into the last merge level)
   const bool multi = c->nranks > 1;
   const MomentsFinalize fin{sigma_multiplier, iter, rules == ICP_RULES_ENGINE ? 1 : 0};
@@ -422,14 +430,31 @@ int icp_hip_iterate(icp_hip_ctx* c, const double* T_apply, int iter, int rules, 
   cl.xcd_remap = c->xcd_remap;
   HIP_TRY(launch_cull_cov(cl, s));
   // covariance moments -> RMSE; the finished record is stored into pinned host memory
-  const IterPublish pub{c->h_it_dev, c->fb_count};
+  const uint64_t seq = ++c->publish_seq;
+  const IterPublish pub{c->h_it_dev, c->fb_count, (double)seq};
   HIP_TRY(launch_merge_cov(c->cparts, c->nb_cull, c->it, multi ? nullptr : &pub, s));
   if (multi) {
     RCCL_TRY(ncclAllGather(&c->it->c_local, c->gc, sizeof(CovMoments) / sizeof(double), ncclDouble, c->comm, s));
     HIP_TRY(launch_finalize_cov(c->gc, c->nranks, c->it, pub, s));
   }
-  HIP_TRY(hipEventRecord(c->ev_it1, s));
-  HIP_TRY(hipStreamSynchronize(s));
+  HIP_TRY(hipEventRecord(ev[3], s));
+  c->n_iterates++;
+  // The host's only wait of the iteration: the publishing kernel's last store is the sequence
+  // number (after a system-scope fence), so the record is complete once it shows up. Polling
+  // the pinned word wakes the host within ~1 us; the stream is queried between polls so a
+  // device error still surfaces.
+  {
+    const volatile double* flag = &c->h_it->pad[3];
+    const double want = (double)seq;
+    for (unsigned spin = 1; *flag != want; spin++) {
+      if ((spin & 1023u) == 0) {
+        const hipError_t q = hipStreamQuery(s);
+        if (q == hipSuccess && *flag == want) break;
+        if (q == hipSuccess) return fail(ICP_HIP_EDEVICE, "iterate: stream idle but the record was not published");
+        if (q != hipErrorNotReady) return fail(ICP_HIP_EDEVICE, std::string("iterate: ") + hipGetErrorString(q));
+      }
+    }
+  }
   c->lists_zero = true;
   for (int k = 0; k < 3; k++) c->last_lists[k] = (unsigned int)c->h_it->pad[k];
   const IterDev& h = *c->h_it;
@@ -561,6 +586,7 @@ int icp_hip_nn(icp_hip_ctx* c, const double* q, int64_t n, int32_t* idx_out, dou
   a.cells = c->cells;
   a.cell_lmax = c->cell_lmax;
   a.xcd_remap = c->xcd_remap;
+  a.ball_groups = c->ball_groups;
   for (int k = 0; k < 3; k++) {
     a.root_lo[k] = c->root_box[k];
     a.root_hi[k] = c->root_box[3 + k];
@@ -621,6 +647,7 @@ int icp_hip_traversal_counts(icp_hip_ctx* c, double* mean_entries, double* mean_
   a.cells = c->cells;
   a.cell_lmax = c->cell_lmax;
   a.xcd_remap = c->xcd_remap;
+  a.ball_groups = c->ball_groups;
   for (int k = 0; k < 3; k++) {
     a.root_lo[k] = c->root_box[k];
     a.root_hi[k] = c->root_box[3 + k];
@@ -645,15 +672,26 @@ int icp_hip_target_info(icp_hip_ctx* c, int64_t* n_nodes, int64_t* n_leaves, int
   return ICP_HIP_OK;
 }
 
+int icp_hip_timings(icp_hip_ctx* c, int k, double* nn_ms, double* it_ms) {
+  if (!c || k < 0) return fail(ICP_HIP_EINVAL, "bad arguments");
+  if (k > icp_hip_ctx::kTimingRing || k > c->n_iterates) return fail(ICP_HIP_EINVAL, "fewer iterates recorded than asked");
+  HIP_TRY(hipSetDevice(c->device));
+  for (int j = 0; j < k; j++) {
+    hipEvent_t* ev = c->ring[(c->n_iterates - k + j) % icp_hip_ctx::kTimingRing];
+    HIP_TRY(hipEventSynchronize(ev[3]));
+    float a = 0.f, b = 0.f;
+    HIP_TRY(hipEventElapsedTime(&a, ev[1], ev[2]));
+    HIP_TRY(hipEventElapsedTime(&b, ev[0], ev[3]));
+    if (nn_ms) nn_ms[j] = a;
+    if (it_ms) it_ms[j] = b;
+  }
+  return ICP_HIP_OK;
+}
+
 int icp_hip_last_timing(icp_hip_ctx* c, double* nn_ms, double* it_ms) {
   if (!c) return fail(ICP_HIP_EINVAL, "null ctx");
-  HIP_TRY(hipSetDevice(c->device));
-  float a = 0.f, b = 0.f;
-  HIP_TRY(hipEventElapsedTime(&a, c->ev_nn0, c->ev_nn1));
-  HIP_TRY(hipEventElapsedTime(&b, c->ev_it0, c->ev_it1));
-  if (nn_ms) *nn_ms = a;
-  if (it_ms) *it_ms = b;
-  return ICP_HIP_OK;
+  if (c->n_iterates == 0) return fail(ICP_HIP_ENOTREADY, "no iterate has run");
+  return icp_hip_timings(c, 1, nn_ms, it_ms);
 }
 
 int icp_hip_synchronize(icp_hip_ctx* c) {

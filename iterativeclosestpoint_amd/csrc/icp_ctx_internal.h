@@ -16,9 +16,15 @@ struct icp_hip_ctx {
   int scan32 = 1;         // fp32 filter scan in the wave search (ICP_SCAN32=0: fp64 scan)
   int lca_descent = 1;    // uniform descent before the wave's breadth-first walk (ICP_LCA=0: off)
   int use_cells = 1;      // start the wave walk from the cell tables (ICP_CELLS=0: off)
+  int ball_groups = 4;    // queries per wave of the ball search (ICP_BALL_GROUPS=1: one)
   int xcd_remap = 0;      // XCD-contiguous block order for search and cull (ICP_XCD=1; measured: no gain)
   hipStream_t stream = nullptr;
-  hipEvent_t ev_it0 = nullptr, ev_it1 = nullptr, ev_nn0 = nullptr, ev_nn1 = nullptr;
+  hipEvent_t ev_it0 = nullptr, ev_it1 = nullptr;  // set_target timing
+  // per-iterate timing events, a ring over the last kTimingRing iterates:
+  // [0] iterate start, [1] search start, [2] search kernel done, [3] iterate end
+  static constexpr int kTimingRing = 64;
+  hipEvent_t ring[kTimingRing][4] = {};
+  int64_t n_iterates = 0;
 
   // target (replicated on every rank)
   icp::NodeRec* nodes = nullptr;
@@ -54,6 +60,7 @@ struct icp_hip_ctx {
   icp::IterDev* it = nullptr;
   icp::IterDev* h_it = nullptr;      // pinned, coherent: the publishing kernel stores into it
   icp::IterDev* h_it_dev = nullptr;  // its device address
+  uint64_t publish_seq = 0;          // h_it->pad[3] = seq once the record is complete
   unsigned long long* counters = nullptr;
   double* Tbuf = nullptr;
 

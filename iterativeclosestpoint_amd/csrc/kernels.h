@@ -57,6 +57,7 @@ struct NNLaunch {
   double root_lo[3], root_hi[3];  // root box (the octree's midpoint recursion starts here)
   unsigned long long* dbg; // optional diagnostics of the wave-cooperative search (ICP_NN_DEBUG)
   int xcd_remap;           // variant 4: each XCD takes one contiguous range of query blocks
+  int ball_groups;         // variant 4: queries per wave of the ball search (4; 1 = one per wave)
 };
 
 // Threads per block of the NN kernel for a given stack depth.
@@ -87,6 +88,7 @@ hipError_t launch_finalize_moments(const Moments* gathered, int nranks, IterDev*
 struct IterPublish {
   IterDev* host;
   unsigned int* lists;
+  double seq;  // stored last into host->pad[3]: the record is complete
 };
 
 struct CullLaunch {

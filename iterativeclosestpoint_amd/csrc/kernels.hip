@@ -15,6 +15,8 @@
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
+#include <cstddef>
+
 #include "kernels.h"
 
 namespace icp {
@@ -1617,6 +1619,215 @@ __global__ void __launch_bounds__(64) k_nn_ball(NNLaunch a) {
   }
 }
 
+// The ball search with four queries per wave, one 16-lane group (a DPP row) each: the list's
+// queries are latency-bound walks of a few dependent rounds, so four in flight per wave hide four
+// times the latency of one. Same walk, sphere test and certificate as k_nn_ball per group; the
+// group's candidate list holds 256 points (more: the query goes to the per-lane search).
+constexpr int kBallGroups = 4;
+constexpr int kBallGL = 64 / kBallGroups;         // lanes per query
+constexpr int kBallGStack = kBallStack / kBallGroups;
+constexpr int kBallGPoints = kBallPoints / kBallGroups;
+
+// Inclusive prefix sum within each 16-lane row (row_shr 1, 2, 4, 8); *total = the row's sum.
+__device__ __forceinline__ int row_incl_scan(int v, int row_base, int* total) {
+  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, true);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, true);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, true);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, true);
+  *total = __shfl(v, row_base + 15, kWave);
+  return v;
+}
+
+// cell_starts for one 16-lane group: at most 16 cells (one per lane), paths from the group's
+// first 6 lanes. Writes the start nodes to out[0 .. count) and returns count (group-uniform).
+__device__ __forceinline__ int cell_starts_g(const NNLaunch& a, double blx, double bly, double blz, double bhx,
+                                             double bhy, double bhz, int gl, int gbase, int32_t* out) {
+  int L = a.cell_lmax;
+  uint32_t path = 0;
+  if (gl < 6) {
+    const int ax = gl >> 1;
+    const double v = (gl & 1) ? (ax == 0 ? bhx : ax == 1 ? bhy : bhz) : (ax == 0 ? blx : ax == 1 ? bly : blz);
+    double lo = ax == 0 ? a.root_lo[0] : ax == 1 ? a.root_lo[1] : a.root_lo[2];
+    double hi = ax == 0 ? a.root_hi[0] : ax == 1 ? a.root_hi[1] : a.root_hi[2];
+    for (int l = 0; l < L; l++) {
+      const double m = (lo + hi) / 2;
+      const bool up = v > m;
+      path = 2u * path + (up ? 1u : 0u);
+      lo = up ? m : lo;
+      hi = up ? hi : m;
+    }
+  }
+  uint32_t ilx = (uint32_t)__shfl((int)path, gbase + 0, kWave), ihx = (uint32_t)__shfl((int)path, gbase + 1, kWave);
+  uint32_t ily = (uint32_t)__shfl((int)path, gbase + 2, kWave), ihy = (uint32_t)__shfl((int)path, gbase + 3, kWave);
+  uint32_t ilz = (uint32_t)__shfl((int)path, gbase + 4, kWave), ihz = (uint32_t)__shfl((int)path, gbase + 5, kWave);
+  while (L > 0 && (ihx - ilx + 1) * (ihy - ily + 1) * (ihz - ilz + 1) > (uint32_t)kBallGL) {
+    L--;
+    ilx >>= 1; ihx >>= 1; ily >>= 1; ihy >>= 1; ilz >>= 1; ihz >>= 1;
+  }
+  const uint32_t nx = ihx - ilx + 1, ny = ihy - ily + 1, nz = ihz - ilz + 1;
+  bool put = false;
+  int32_t node = 0;
+  if ((uint32_t)gl < nx * ny * nz) {
+    const uint32_t cx = ilx + (uint32_t)gl % nx, cy = ily + ((uint32_t)gl / nx) % ny, cz = ilz + (uint32_t)gl / (nx * ny);
+    const uint32_t prefix = spread3(cx) | (spread3(cy) << 1) | (spread3(cz) << 2);
+    const int32_t e = a.cells[(((int64_t)1 << (3 * L)) - 1) / 7 + prefix];
+    if (e >= 0) {
+      node = e >> 5;
+      const int sh = L - (e & 31);
+      const uint32_t fx = ((cx >> sh) << sh) > ilx ? ((cx >> sh) << sh) : ilx;
+      const uint32_t fy = ((cy >> sh) << sh) > ily ? ((cy >> sh) << sh) : ily;
+      const uint32_t fz = ((cz >> sh) << sh) > ilz ? ((cz >> sh) << sh) : ilz;
+      put = cx == fx && cy == fy && cz == fz;
+    }
+  }
+  const uint32_t pm = (uint32_t)((__ballot(put) >> gbase) & 0xffffull);
+  if (put) out[__builtin_popcount(pm & ((1u << gl) - 1u))] = node;
+  return __builtin_popcount(pm);
+}
+
+__global__ void __launch_bounds__(64) k_nn_ball4(NNLaunch a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned long long lds_stack[];
+  const int lane = threadIdx.x, g = lane / kBallGL, gl = lane % kBallGL, gbase = g * kBallGL;
+  int32_t* stack = reinterpret_cast<int32_t*>(lds_stack) + g * kBallGStack;
+  int32_t* plist = reinterpret_cast<int32_t*>(lds_stack) + kBallStack + g * kBallGPoints;
+  const unsigned cnt = a.fb_count[1];
+  for (unsigned j0 = blockIdx.x * kBallGroups; j0 < cnt; j0 += gridDim.x * kBallGroups) {
+    const unsigned j = j0 + g;
+    bool live = j < cnt;  // group-uniform
+    int64_t i = 0;
+    double u = 0.0, qx = 0.0, qy = 0.0, qz = 0.0;
+    if (live) {
+      i = a.fb_list2[j];
+      u = a.fb_u2[j];
+      qx = a.x[i];
+      qy = a.y[i];
+      qz = a.z[i];
+      if (!(u <= 0x1p900)) {
+        if (gl == 0) a.fb_list3[atomicAdd(a.fb_count + 2, 1u)] = (int32_t)i;
+        live = false;
+      }
+    }
+    const double thr = u * (1.0 + kFastPrune);
+    int tail = 0, npts = 0;
+    bool overflow = false;
+    wave_lds_fence();
+    {
+      // every point with fl(d2) <= thr lies in the box q +- r (see k_nn4's radius)
+      const double amax = __builtin_fmax(__builtin_fabs(qx), __builtin_fmax(__builtin_fabs(qy), __builtin_fabs(qz)));
+      const double r = live ? __builtin_sqrt(thr) * (1.0 + 0x1p-40) + amax * 0x1p-45 : 0.0;
+      const int t = cell_starts_g(a, qx - r, qy - r, qz - r, qx + r, qy + r, qz + r, gl, gbase, stack);
+      tail = live ? t : 0;
+    }
+    wave_lds_fence();
+    // LIFO batches of up to 16 nodes per group, sphere test s <= thr on the children
+    while (__ballot(tail > 0) != 0) {
+      const int batch = tail < kBallGL ? tail : kBallGL;
+      const bool has = gl < batch;
+      bool leaf = false;
+      int32_t first = 0;
+      uint32_t meta = 0, kids = 0;
+      if (has) {
+        const NodeRec* rr = a.nodes + stack[tail - batch + gl];
+        const int2 topo = *reinterpret_cast<const int2*>(&rr->first);
+        first = topo.x;
+        meta = (uint32_t)topo.y;
+        leaf = (meta & kLeafBit) != 0;
+        if (!leaf) {
+          const double2 l01 = *reinterpret_cast<const double2*>(&rr->lo[0]);
+          const double2 l2h0 = *reinterpret_cast<const double2*>(&rr->lo[2]);
+          const double2 h12 = *reinterpret_cast<const double2*>(&rr->hi[1]);
+          const double lx = l01.x, ly = l01.y, lz = l2h0.x, hx = l2h0.y, hy = h12.x, hz = h12.y;
+          const double mx = (lx + hx) / 2, my = (ly + hy) / 2, mz = (lz + hz) / 2;
+          const double ax0 = smax(0.0, smax(lx - qx, qx - mx)), ax1 = smax(0.0, smax(mx - qx, qx - hx));
+          const double ay0 = smax(0.0, smax(ly - qy, qy - my)), ay1 = smax(0.0, smax(my - qy, qy - hy));
+          const double az0 = smax(0.0, smax(lz - qz, qz - mz)), az1 = smax(0.0, smax(mz - qz, qz - hz));
+          const double sx[2] = {ax0 * ax0, ax1 * ax1};
+          const double sy[2] = {ay0 * ay0, ay1 * ay1};
+          const double sz[2] = {az0 * az0, az1 * az1};
+          const uint32_t mask = meta & 0xffu;
+#pragma unroll
+          for (int o = 0; o < 8; o++) {
+            const double c = sx[o & 1] + sy[(o >> 1) & 1] + sz[o >> 2];
+            kids |= (((mask >> o) & 1u) && !(c > thr)) ? (1u << o) : 0u;
+          }
+        }
+      }
+      const int lcnt = (has && leaf) ? (int)(meta & ~kLeafBit) : 0;
+      int ltot;
+      const int lincl = row_incl_scan(lcnt, gbase, &ltot);
+      const int lpos = npts + lincl - lcnt;
+      if (lcnt > 0 && lpos + lcnt <= kBallGPoints)
+        for (int c = 0; c < lcnt; c++) plist[lpos + c] = first + c;
+      const int nch = __builtin_popcount(kids);
+      int tot;
+      const int incl = row_incl_scan(nch, gbase, &tot);
+      if (tail > 0) {
+        npts += ltot;
+        tail -= batch;
+        if (npts > kBallGPoints || tail + tot > kBallGStack) {
+          overflow = true;
+          tail = 0;
+        } else {
+          int off = tail + incl - nch;
+          const uint32_t mask = meta & 0xffu;
+          uint32_t kk = kids;
+          while (kk) {
+            const uint32_t o = (uint32_t)__builtin_ctz(kk);
+            kk &= kk - 1u;
+            stack[off++] = first + __builtin_popcount(mask & ((1u << o) - 1u));
+          }
+          tail += tot;
+        }
+      }
+      wave_lds_fence();
+    }
+    if (live && overflow && gl == 0) a.fb_list3[atomicAdd(a.fb_count + 2, 1u)] = (int32_t)i;
+    if (overflow) live = false;
+    wave_lds_fence();
+    double best = __builtin_inf(), second = __builtin_inf();
+    int32_t bpos = 0x7fffffff;
+    if (live) {
+      for (int k = gl; k < npts; k += kBallGL) {
+        const int32_t pg = plist[k];
+        const TgtPt* p = a.pts + pg;
+        const double2 xy = *reinterpret_cast<const double2*>(&p->x);
+        const double dx = xy.x - qx, dy = xy.y - qy, dz = p->z - qz;
+        const double d2 = dx * dx + dy * dy + dz * dz;
+        if (d2 < best) {
+          second = best;
+          best = d2;
+          bpos = pg;
+        } else if (d2 < second) {
+          second = d2;
+        }
+      }
+    }
+#pragma unroll
+    for (int o = kBallGL / 2; o >= 1; o >>= 1) {
+      const double ob = __shfl_xor(best, o, kWave);
+      const double os = __shfl_xor(second, o, kWave);
+      const int32_t op = __shfl_xor(bpos, o, kWave);
+      const double lo_ = ob < best ? ob : best;
+      const double hi_ = ob < best ? best : ob;
+      const double ss = os < second ? os : second;
+      second = hi_ < ss ? hi_ : ss;
+      bpos = (ob < best || (ob == best && op < bpos)) ? op : bpos;
+      best = lo_;
+    }
+    if (live && gl == 0) {
+      if (!(best <= u)) {
+        a.fb_list3[atomicAdd(a.fb_count + 2, 1u)] = (int32_t)i;
+      } else if (certified(best, second, a.init_best)) {
+        a.pos_out[i] = bpos;
+        a.dist_out[i] = __builtin_sqrt(best);
+      } else {
+        a.fb_list[atomicAdd(a.fb_count, 1u)] = (int32_t)i;
+      }
+    }
+    wave_lds_fence();
+  }
+}
+
 // Per-lane certified search over the queries the ball search left (compacted: full waves).
 __global__ void __launch_bounds__(256) k_nn3_list(NNLaunch a) {
   extern __shared__ __attribute__((aligned(16))) unsigned long long lds_stack[];
@@ -1733,15 +1944,21 @@ __device__ void finalize_cov_publish(IterDev* it, const CovMoments& g, IterPubli
       rec->pad[k] = (double)pub.lists[k];
       pub.lists[k] = 0u;
     }
-    rec->pad[3] = 0.0;
     it->c_global = rec->c_global;
     it->rmse = rec->rmse;
   }
   __syncthreads();
   const double* src = reinterpret_cast<const double*>(rec);
   double* dst = reinterpret_cast<double*>(pub.host);
-  for (int k = threadIdx.x; k < (int)(sizeof(IterDev) / sizeof(double)); k += blockDim.x) dst[k] = src[k];
+  constexpr int kWords = (int)(sizeof(IterDev) / sizeof(double)) - 1;  // all but pad[3], the flag
+  static_assert(offsetof(IterDev, pad) + 3 * sizeof(double) == kWords * sizeof(double), "flag is the last word");
+  for (int k = threadIdx.x; k < kWords; k += blockDim.x) dst[k] = src[k];
   __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    *reinterpret_cast<volatile double*>(&pub.host->pad[3]) = pub.seq;
+    __threadfence_system();
+  }
 }
 
 __global__ void __launch_bounds__(256) k_merge_cov_last(const CovMoments* in, int64_t n, IterDev* it, IterPublish pub,
@@ -1988,7 +2205,12 @@ hipError_t launch_nn(const NNLaunch& a_in, hipStream_t s) {
     const size_t lshm = (size_t)levels * 64 * sizeof(unsigned long long) < 1024 ? 1024
                         : (size_t)levels * 64 * sizeof(unsigned long long);
     const unsigned bgrid = (unsigned)((a.n < 16384) ? a.n : 16384);
-    hipLaunchKernelGGL(k_nn_ball, dim3(bgrid), dim3(64), kBallLdsBytes, s, a);
+    if (a.cells && a.ball_groups != 1)
+      hipLaunchKernelGGL(k_nn_ball4, dim3((unsigned)((a.n + kBallGroups - 1) / kBallGroups < 8192
+                                                     ? (a.n + kBallGroups - 1) / kBallGroups : 8192)),
+                         dim3(64), kBallLdsBytes, s, a);
+    else
+      hipLaunchKernelGGL(k_nn_ball, dim3(bgrid), dim3(64), kBallLdsBytes, s, a);
     hipLaunchKernelGGL(k_nn3_list, dim3(lgrid), dim3(64), lshm, s, a);
     hipLaunchKernelGGL(k_nn_fallback, dim3(lgrid), dim3(64), lshm, s, a);
     return hipGetLastError();
@@ -2058,7 +2280,7 @@ hipError_t launch_merge_cov(const CovMoments* part, int64_t nparts, IterDev* it,
                             hipStream_t s) {
   const CovMoments* cur = merge_to_last_span<CovMoments, d_cov_merge, d_cov_identity>(part, &nparts, s);
   hipLaunchKernelGGL(k_merge_cov_last, dim3(1), dim3(256), 0, s, cur, nparts, it,
-                     pub ? *pub : IterPublish{nullptr, nullptr}, pub ? 1 : 0);
+                     pub ? *pub : IterPublish{nullptr, nullptr, 0.0}, pub ? 1 : 0);
   return hipGetLastError();
 }
 

@@ -237,7 +237,7 @@ def _with_env(env: dict, fn):
 @pytest.mark.parametrize("n,env", [(300_000, {"ICP_SCAN32": "0"}), (1_000_000, {"ICP_SCAN32": "0"}),
                                    (1_000_000, {"ICP_LCA": "0"}), (300_000, {"ICP_SCAN32": "0", "ICP_LCA": "0"}),
                                    (1_000_000, {"ICP_CELLS": "0"}), (300_000, {"ICP_CELLS": "0", "ICP_LCA": "0"}),
-                                   (1_000_000, {"ICP_XCD": "1"})])
+                                   (1_000_000, {"ICP_XCD": "1"}), (1_000_000, {"ICP_BALL_GROUPS": "1"})])
 def test_scan32_matches_fp64_scan(icp, n, env):
     """The fp32 filter scan of the wave search (fp64 winner + rigorous lower bound certificate)
     returns exactly the fp64 scan's correspondences and residuals, iteration after iteration of
