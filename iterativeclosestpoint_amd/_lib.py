@@ -10,7 +10,7 @@ import numpy as np
 
 PKG_DIR = Path(__file__).resolve().parent
 REPO_DIR = PKG_DIR.parent
-LIB_PATH = PKG_DIR / "libicp_hip.so"
+LIB_PATH = Path(os.environ.get("ICP_HIP_LIB", PKG_DIR / "libicp_hip.so"))  # override: A/B of builds
 
 RULES_ENGINE = 0
 RULES_CLI = 1
