@@ -127,7 +127,9 @@ def main() -> int:
     lo, hi = shard_range(n, rank, world)
     ctx = icp.Context(device)
     ctx.set_target(tgt, 10, 20, icp.RULES_ENGINE)
-    ctx.set_source(src[lo:hi])
+    # spatial shards: contiguous ranges of the kd order (a contiguous range of the shuffled cloud
+    # would thin each rank's queries `world` times; see icp_host.h icp_source_shard_order)
+    ctx.set_source(src[icp.source_shard_order(src)[lo:hi]] if world > 1 else src)
     if world > 1:
         uid = [icp.Context.unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
@@ -210,8 +212,8 @@ def main() -> int:
                 "workload": f"{CONFIG_NAMES.get(n, 'custom')}: {n}<->{n} synthetic pair, full ICP iteration "
                             f"(engine rules, octree leaf 10 / depth 20), "
                             f"source sharded over {world} GPU(s), target octree replicated",
-                "n_target": n, "n_source": n, "parallelism": f"source-shard x{world} (RCCL all-gather of 2 "
-                "moment records per iteration)",
+                "n_target": n, "n_source": n, "parallelism": f"spatial source shards x{world} (kd-order ranges; "
+                "RCCL all-gather of 2 moment records per iteration)",
                 "octree_nodes": info["n_nodes"], "octree_leaves": info["n_leaves"],
             },
             "roofline": {

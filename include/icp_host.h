@@ -44,6 +44,14 @@ void icp_cov_from_pairs(const double* a_xyz, const double* b_xyz, const double* 
 void icp_cov_merge(const double* parts20, int32_t nparts, double out20[20]);
 double icp_cull_threshold(double mean, double sd, double k_sigma, int iter, int engine_rules);
 
+/* Spatial sharding of the source for the multi-GPU path: order[] = a permutation of 0..n-1 in
+ * which every contiguous range is spatially compact (kd buckets, the query order of the search
+ * kernel). Rank r of W takes the points order[lo_r .. hi_r) of the balanced contiguous split, so
+ * its queries keep the full density of the cloud (a strided or shuffled split would thin them W
+ * times and every search box would hold W times more target points). Returns 0, or -1 on bad
+ * arguments. No reference counterpart: the reference has one CPU thread and no sharding. */
+int icp_source_shard_order(const double* xyz, int64_t n, int32_t* order);
+
 typedef struct icp_synth_spec {
   double sigma[3];        /* target ~ N(0, diag(sigma^2)), default (5, 5, 1) m           */
   double yaw_deg, pitch_deg, roll_deg; /* R = Rz(yaw) Ry(pitch) Rx(roll), test_icp.cpp:165-189 */

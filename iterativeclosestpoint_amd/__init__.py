@@ -15,6 +15,7 @@ from ._lib import (  # noqa: F401
     params_default,
     engine_register,
     cli_icp,
+    source_shard_order,
     synth_pair,
     octree_build,
     jacobi_svd3,

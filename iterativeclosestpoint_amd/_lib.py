@@ -158,6 +158,7 @@ SIGNATURES = {
     "icp_cull_threshold": (C.c_double, [C.c_double, C.c_double, C.c_double, C.c_int, C.c_int]),
     "icp_synth_default": (None, [C.POINTER(SynthSpec)]),
     "icp_synth_pair": (C.c_int, [C.POINTER(SynthSpec), C.c_int64, C.c_int64, _P, _P, _P]),
+    "icp_source_shard_order": (C.c_int, [_P, C.c_int64, _P]),
     # icp_las.h
     "icp_las_read_header": (C.c_int, [C.c_char_p, C.c_int, C.POINTER(LasHeader)]),
     "icp_las_read": (C.c_int64, [C.c_char_p, C.c_int, C.c_int64, _P, C.POINTER(LasHeader)]),
@@ -426,6 +427,17 @@ def cli_icp(src, tgt, max_iterations=20, tolerance=1e-2, device: int = -1):
     _check(lib().icp_cli_icp(_ptr(src), src.shape[0], _ptr(tgt), tgt.shape[0], max_iterations, tolerance, _ptr(R),
                              _ptr(t), _ptr(tr), cap, C.byref(n), device))
     return R.reshape(3, 3), t, tr[: n.value].reshape(-1, 4, 4), src
+
+
+def source_shard_order(xyz: np.ndarray) -> np.ndarray:
+    """Permutation whose contiguous ranges are spatially compact (icp_source_shard_order): rank r
+    of W takes xyz[order[lo:hi]] for its balanced contiguous range."""
+    xyz = np.ascontiguousarray(xyz, dtype=np.float64)
+    order = np.empty(len(xyz), np.int32)
+    rc = lib().icp_source_shard_order(_ptr(xyz), len(xyz), _ptr(order))
+    if rc != 0:
+        raise IcpError(rc, lib().icp_hip_last_error().decode())
+    return order
 
 
 def synth_pair(n_tgt: int, n_src: int | None = None, **overrides):

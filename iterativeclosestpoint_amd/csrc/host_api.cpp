@@ -7,6 +7,7 @@
 #include "icp_common.h"
 #include "icp_ctx_internal.h"
 #include "octree_build.h"
+#include "query_order.h"
 
 struct icp_octree {
   icp::FlatOctree t;
@@ -184,6 +185,17 @@ void icp_synth_default(icp_synth_spec* s) {
   s->outlier_fraction = 0.01;
   s->seed_target = 42;
   s->seed_source = 43;
+}
+
+int icp_source_shard_order(const double* xyz, int64_t n, int32_t* order) {
+  if (n < 0 || (n > 0 && (!xyz || !order)) || n > (int64_t)0x7fffffff) {
+    icp_ctx_set_error("icp_source_shard_order: bad arguments");
+    return -1;
+  }
+  std::vector<int32_t> perm;
+  icp::kd_query_order(xyz, n, 8, &perm);
+  std::memcpy(order, perm.data(), sizeof(int32_t) * (size_t)n);
+  return 0;
 }
 
 int icp_synth_pair(const icp_synth_spec* s, int64_t n_tgt, int64_t n_src, double* tgt, double* src, double T_true[16]) {

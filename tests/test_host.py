@@ -151,3 +151,23 @@ def test_params_default_mirror_reference(icp):
     p = icp.params_default()
     assert (p.max_iterations, p.tolerance, p.sigma_multiplier, p.octree_max_points, p.octree_max_depth) == \
         (50, 1e-6, 3.0, 10, 20)  # ICPParameters, icpengine.h:13-19
+
+
+def test_source_shard_order_is_a_spatial_permutation(icp):
+    """Contiguous ranges of icp_source_shard_order are spatially compact: 8 shards of a shuffled
+    cloud cover far less volume each than 8 plain ranges (which span the whole cloud)."""
+    import sys
+    from pathlib import Path
+    sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+    from bench import shard_range
+    _, src, _ = icp.synth_pair(200_000)
+    order = icp.source_shard_order(src)
+    assert order.dtype == np.int32 and np.array_equal(np.sort(order), np.arange(len(src)))
+    vol_kd, vol_plain = 0.0, 0.0
+    for r in range(8):
+        lo, hi = shard_range(len(src), r, 8)
+        a, b = src[order[lo:hi]], src[lo:hi]
+        a, b = a[np.all(np.abs(a) < 30, 1)], b[np.all(np.abs(b) < 30, 1)]  # outliers aside
+        vol_kd += np.prod(np.percentile(a, 95, 0) - np.percentile(a, 5, 0))
+        vol_plain += np.prod(np.percentile(b, 95, 0) - np.percentile(b, 5, 0))
+    assert vol_kd < 0.4 * vol_plain

@@ -1,0 +1,40 @@
+"""Per-rank cost of one ICP iteration at world size W, probed on one GPU (no collectives): the
+full 10M target, rank 0's source shard (spatial: a kd-order range; SPATIAL=0: a plain range of the
+shuffled cloud). Estimates the strong-scaling floor of bench.py --gpus W
+(the real run adds two RCCL all-gathers of one record per iteration)."""
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np
+
+import iterativeclosestpoint_amd as icp
+from bench import shard_range
+
+n = int(os.environ.get("N", "10000000"))
+worlds = [int(w) for w in (sys.argv[1] if len(sys.argv) > 1 else "1,2,4,8").split(",")]
+tgt, src, _ = icp.synth_pair(n)
+ctx = icp.Context(0)
+ctx.set_target(tgt, 10, 20, icp.RULES_ENGINE)
+order = icp.source_shard_order(src) if os.environ.get("SPATIAL", "1") == "1" else np.arange(n)
+for w in worlds:
+    lo, hi = shard_range(n, 0, w)
+    ctx.set_source(src[order[lo:hi]])
+    sess = ctx.session(icp.params_default(max_iterations=20, tolerance=1e-6, flags=icp.FLAG_NO_EARLY_STOP))
+    for _ in range(3):
+        sess.step()
+    ctx.synchronize()
+    k = 10
+    t0 = time.perf_counter()
+    for _ in range(k):
+        sess.step()
+    ctx.synchronize()
+    dt = (time.perf_counter() - t0) / k
+    nn, it = ctx.timings(k)
+    print(json.dumps({"world": w, "shard": hi - lo, "ms_per_step": round(dt * 1e3, 4),
+                      "knn_ms": round(float(np.mean(nn)), 4), "iter_device_ms": round(float(np.mean(it)), 4),
+                      "est_mcorr_s": round(n / dt / 1e6, 1)}), flush=True)
+    sess.finish()
+ctx.close()
