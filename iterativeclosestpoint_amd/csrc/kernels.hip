@@ -845,7 +845,7 @@ __global__ void __launch_bounds__(256) k_moments(const double* __restrict__ dist
 // lane's ball of radius r lies in B, so every point with fl(d2) <= best (1 + 2^-48) is among
 // the scanned ones and the window certificate of k_nn3 applies unchanged. Lanes that do not
 // join (outliers: far from the surface, or a wave whose candidate set overflows LDS) are queued
-// for the per-lane certified search (k_nn3_list); uncertified ones for the exact DFS.
+// for the per-lane certified search (k_nn_lists); uncertified ones for the exact DFS.
 
 // Workgroups are dispatched round-robin over the 8 XCDs (blockIdx % 8 labels the blocks that share
 // one XCD and its 4 MB L2; cdna_hip_programming.md T1). Renumbered so that each such set takes
@@ -1476,7 +1476,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
 // tighter than k_nn4's box — and scans their points one per lane. Certification as in k_nn4
 // (best <= u and the window test). Leaves of boxes with s > u (1 + 2^-47) only hold points with
 // fl(d2) > best (1 + 2^-48) (monotone rounding, see k_nn3), so nothing in the window is missed.
-// No usable guess or an overflowing candidate set -> per-lane search (k_nn3_list).
+// No usable guess or an overflowing candidate set -> per-lane search (k_nn_lists).
 constexpr int kBallStack = 512;
 constexpr int kBallPoints = 1024;
 constexpr int kBallLdsBytes = kBallStack * 4 + kBallPoints * 4;
@@ -1828,45 +1828,52 @@ __global__ void __launch_bounds__(64) k_nn_ball4(NNLaunch a) {
   }
 }
 
-// Per-lane certified search over the queries the ball search left (compacted: full waves).
-__global__ void __launch_bounds__(256) k_nn3_list(NNLaunch a) {
+
+// The two short lists the ball search leaves, in one launch: thread j < n3 takes lane-list entry
+// j (per-lane certified search; a query it cannot certify gets the reference-order DFS right
+// away, in the same thread), the rest take the exact list (queries k_nn4 or the ball search could
+// not certify). Both lists are complete when this kernel starts; it appends nothing.
+__global__ void __launch_bounds__(64) k_nn_lists(NNLaunch a) {
   extern __shared__ __attribute__((aligned(16))) unsigned long long lds_stack[];
-  const unsigned cnt = a.fb_count[2];
-  for (unsigned j0 = blockIdx.x * blockDim.x; j0 < cnt; j0 += gridDim.x * blockDim.x) {
-    const unsigned j = j0 + threadIdx.x;
-    const bool act = j < cnt;
-    const int64_t i = act ? a.fb_list3[j] : 0;
-    bool ok = false;
-    if (act) {
-      const double qx = a.x[i], qy = a.y[i], qz = a.z[i];
+  const unsigned n3 = a.fb_count[2], n0 = a.fb_count[0];
+  for (unsigned j = blockIdx.x * blockDim.x + threadIdx.x; j < n3 + n0; j += gridDim.x * blockDim.x) {
+    const bool lane_list = j < n3;
+    const int64_t i = lane_list ? a.fb_list3[j] : a.fb_list[j - n3];
+    const double qx = a.x[i], qy = a.y[i], qz = a.z[i];
+    if (lane_list) {
       double best = __builtin_inf(), second = __builtin_inf();
       int32_t bpos = -1;
       uint32_t nvis = 0, npts = 0;
       fast_dfs(a, qx, qy, qz, lds_stack + threadIdx.x, blockDim.x, best, second, bpos, nvis, npts);
-      ok = certified(best, second, a.init_best);
-      if (a.dbg) {
-        atomicAdd(&a.dbg[8], (unsigned long long)nvis);
-        atomicMax(&a.dbg[9], (unsigned long long)nvis);
-        atomicAdd(&a.dbg[10], (unsigned long long)npts);
-        if (nvis > 256) atomicAdd(&a.dbg[11], 1ull);
-        if (nvis > 1024) atomicAdd(&a.dbg[12], 1ull);
-        atomicMax(&a.dbg[13], (unsigned long long)__builtin_sqrt(best) * 1000ull);
-      }
-      if (ok) {
+      if (certified(best, second, a.init_best)) {
         a.pos_out[i] = bpos;
         a.dist_out[i] = __builtin_sqrt(best);
+        continue;
       }
     }
-    wave_append(act && !ok, i, a.fb_count, a.fb_list);
+    double best_d2 = a.init_best, visits = 0.0, scanned = 0.0;
+    int32_t best = -1;
+    exact_dfs<false>(a, qx, qy, qz, lds_stack + threadIdx.x, blockDim.x, best, best_d2, visits, scanned);
+    int32_t pos = best;
+    double d;
+    if (best >= 0) {
+      d = __builtin_sqrt(best_d2);
+    } else {
+      pos = a.pos0;
+      const TgtPt p = a.pts[pos];
+      const double dx = qx - p.x, dy = qy - p.y, dz = qz - p.z;
+      d = __builtin_sqrt(dx * dx + dy * dy + dz * dz);
+    }
+    a.pos_out[i] = pos;
+    a.dist_out[i] = d;
   }
 }
 
 // Fixed-shape merges of block partials (Chan et al. pairwise formulas), deterministic: the same
 // n always gives the same merge tree. Inner levels: block b merges items [256 b, 256 b + 256),
-// one per thread, pairwise in LDS. Last level: one block, up to 1024 items, thread t merges items
-// 4t..4t+3 as ((0, 1), (2, 3)), then the block's pairwise tree. Every load is independent: no
-// dependent chain longer than log2 of the items.
-constexpr int kLastSpan = 1024;
+// one per thread, pairwise in LDS. Last level: one block, up to 4096 items, thread t merges its
+// 16 consecutive items pairwise (quads, then quads of quads), then the block's pairwise tree.
+constexpr int kLastSpan = 4096;
 
 template <typename T, T (*Merge)(const T&, const T&), T (*Identity)()>
 __device__ __forceinline__ T block_tree(T v, T* sm) {
@@ -1881,13 +1888,22 @@ __device__ __forceinline__ T block_tree(T v, T* sm) {
 }
 
 template <typename T, T (*Merge)(const T&, const T&), T (*Identity)()>
-__device__ __forceinline__ T block_tree_last(const T* in, int64_t n, T* sm) {
-  const int64_t g = 4 * (int64_t)threadIdx.x;
+__device__ __forceinline__ T block_quad(const T* in, int64_t n, int64_t g) {
   const T i0 = g < n ? in[g] : Identity();
   const T i1 = g + 1 < n ? in[g + 1] : Identity();
   const T i2 = g + 2 < n ? in[g + 2] : Identity();
   const T i3 = g + 3 < n ? in[g + 3] : Identity();
-  return block_tree<T, Merge, Identity>(Merge(Merge(i0, i1), Merge(i2, i3)), sm);
+  return Merge(Merge(i0, i1), Merge(i2, i3));
+}
+
+template <typename T, T (*Merge)(const T&, const T&), T (*Identity)()>
+__device__ __forceinline__ T block_tree_last(const T* in, int64_t n, T* sm) {
+  // thread t: items 16t .. 16t + 15 as ((q0, q1), (q2, q3)) of quads ((0, 1), (2, 3))
+  // (no early exit: block_tree's barriers must be reached by every thread in uniform control flow)
+  const int64_t g = 16 * (int64_t)threadIdx.x;
+  const T q01 = Merge(block_quad<T, Merge, Identity>(in, n, g), block_quad<T, Merge, Identity>(in, n, g + 4));
+  const T q23 = Merge(block_quad<T, Merge, Identity>(in, n, g + 8), block_quad<T, Merge, Identity>(in, n, g + 12));
+  return block_tree<T, Merge, Identity>(Merge(q01, q23), sm);
 }
 
 __device__ Moments d_moments_merge(const Moments& a, const Moments& b) { return moments_merge(a, b); }
@@ -2211,8 +2227,7 @@ hipError_t launch_nn(const NNLaunch& a_in, hipStream_t s) {
                          dim3(64), kBallLdsBytes, s, a);
     else
       hipLaunchKernelGGL(k_nn_ball, dim3(bgrid), dim3(64), kBallLdsBytes, s, a);
-    hipLaunchKernelGGL(k_nn3_list, dim3(lgrid), dim3(64), lshm, s, a);
-    hipLaunchKernelGGL(k_nn_fallback, dim3(lgrid), dim3(64), lshm, s, a);
+    hipLaunchKernelGGL(k_nn_lists, dim3(lgrid), dim3(64), lshm, s, a);
     return hipGetLastError();
   }
   if (a.variant == 3 && !a.count) {
