@@ -147,13 +147,13 @@ def main() -> int:
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        sess.step()
+    taken = sess.step_n(args.steps)  # the engine's own loop, K iterations (no early stop)
     ctx.synchronize()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    assert taken == args.steps, f"only {taken} of {args.steps} iterations ran"
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

@@ -107,6 +107,9 @@ typedef struct icp_session icp_session;
 int icp_session_create(icp_hip_ctx* ctx, const icp_params* p, const icp_engine_hooks* hooks, icp_session** out);
 /* rec (optional) receives the record of this iteration when one is produced (*produced = 1). */
 int icp_session_step(icp_session* s, icp_iteration_record* rec, int32_t* produced, int32_t* done);
+/* Up to k steps in one call (no records returned; hooks still fire); stops early when the loop
+ * is done. *steps_done = steps taken. Same as calling icp_session_step k times. */
+int icp_session_step_n(icp_session* s, int32_t k, int32_t* steps_done, int32_t* done);
 int icp_session_finish(icp_session* s, icp_result* res);
 /* Current cumulative transform (row-major 4x4). */
 void icp_session_transform(const icp_session* s, double T_cum[16]);

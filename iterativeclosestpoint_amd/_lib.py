@@ -136,6 +136,7 @@ SIGNATURES = {
                                  C.c_int32, C.POINTER(Hooks)]),
     "icp_session_create": (C.c_int, [_P, C.POINTER(Params), C.POINTER(Hooks), C.POINTER(C.c_void_p)]),
     "icp_session_step": (C.c_int, [_P, C.POINTER(IterationRecord), _I32, _I32]),
+    "icp_session_step_n": (C.c_int, [_P, C.c_int32, _I32, _I32]),
     "icp_session_finish": (C.c_int, [_P, C.POINTER(Result)]),
     "icp_session_transform": (None, [_P, _P]),
     "icp_session_destroy": (None, [_P]),
@@ -372,6 +373,20 @@ class Session:
         self.done = bool(done.value)
         _check(rc)
         return rec if produced.value else None
+
+    def step_n(self, k: int) -> int:
+        """Up to k steps in one native call (no records); returns the steps taken."""
+        if not hasattr(lib(), "icp_session_step_n"):  # an older build under A/B
+            taken = 0
+            while taken < k and not self.done:
+                self.step()
+                taken += 1
+            return taken
+        n, done = C.c_int32(0), C.c_int32(0)
+        rc = lib().icp_session_step_n(self._h, k, C.byref(n), C.byref(done))
+        self.done = bool(done.value)
+        _check(rc)
+        return n.value
 
     def transform(self) -> np.ndarray:
         T = np.empty(16)

@@ -243,6 +243,20 @@ int icp_session_step(icp_session* s, icp_iteration_record* rec, int32_t* produce
   return finish_step(false);
 }
 
+int icp_session_step_n(icp_session* s, int32_t k, int32_t* steps_done, int32_t* done) {
+  if (!s || k < 0) return ICP_HIP_EINVAL;
+  int32_t n = 0, d = 0;
+  int rc = ICP_HIP_OK;
+  while (n < k && !d) {
+    rc = icp_session_step(s, nullptr, nullptr, &d);
+    if (rc != ICP_HIP_OK) break;
+    n++;
+  }
+  if (steps_done) *steps_done = n;
+  if (done) *done = d;
+  return rc;
+}
+
 int icp_session_finish(icp_session* s, icp_result* res) {
   if (!s || !res) return ICP_HIP_EINVAL;
   std::memset(res, 0, sizeof(*res));

@@ -28,8 +28,7 @@ for w in worlds:
     ctx.synchronize()
     k = 10
     t0 = time.perf_counter()
-    for _ in range(k):
-        sess.step()
+    sess.step_n(k)
     ctx.synchronize()
     dt = (time.perf_counter() - t0) / k
     nn, it = ctx.timings(k)
