@@ -411,8 +411,8 @@ int icp_hip_iterate(icp_hip_ctx* c, const double* T_apply, int iter, int rules, 
   // residual moments -> mean, std, threshold (one rank: fused into the last merge level)
   const bool multi = c->nranks > 1;
   const MomentsFinalize fin{sigma_multiplier, iter, rules == ICP_RULES_ENGINE ? 1 : 0};
-  HIP_TRY(launch_moments(c->dist, c->n_src, c->mparts, s));
-  HIP_TRY(launch_merge_moments(c->mparts, c->nb_mom, c->it, multi ? nullptr : &fin, s));
+  HIP_TRY(launch_moments(c->dist, c->n_src, c->it, c->mparts, s));
+  HIP_TRY(launch_merge_moments(c->mparts, c->nb_mom, c->dist, c->n_src, c->it, multi ? nullptr : &fin, s));
   if (multi) {
     RCCL_TRY(ncclAllGather(&c->it->m_local, c->gm, sizeof(Moments) / sizeof(double), ncclDouble, c->comm, s));
     HIP_TRY(launch_finalize_moments(c->gm, c->nranks, c->it, fin, s));
@@ -432,7 +432,7 @@ int icp_hip_iterate(icp_hip_ctx* c, const double* T_apply, int iter, int rules, 
   // covariance moments -> RMSE; the finished record is stored into pinned host memory
   const uint64_t seq = ++c->publish_seq;
   const IterPublish pub{c->h_it_dev, c->fb_count, (double)seq};
-  HIP_TRY(launch_merge_cov(c->cparts, c->nb_cull, c->it, multi ? nullptr : &pub, s));
+  HIP_TRY(launch_merge_cov(c->cparts, c->nb_cull, cl, c->it, multi ? nullptr : &pub, s));
   if (multi) {
     RCCL_TRY(ncclAllGather(&c->it->c_local, c->gc, sizeof(CovMoments) / sizeof(double), ncclDouble, c->comm, s));
     HIP_TRY(launch_finalize_cov(c->gc, c->nranks, c->it, pub, s));

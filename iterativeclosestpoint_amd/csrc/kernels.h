@@ -67,7 +67,7 @@ hipError_t launch_nn(const NNLaunch& a, hipStream_t s);
 
 // Residual moments of the settled queries in fixed parts (deterministic), then the merges.
 int64_t moments_num_parts(int64_t n);
-hipError_t launch_moments(const double* dist, int64_t n, Moments* part, hipStream_t s);
+hipError_t launch_moments(const double* dist, int64_t n, const IterDev* it, Moments* part, hipStream_t s);
 // Partial buffers need merge_scratch_entries(nparts) entries of fold scratch behind the partials.
 int64_t merge_scratch_entries(int64_t nparts);
 
@@ -77,8 +77,8 @@ struct MomentsFinalize {
   int engine_rules;
 };
 // Merge the rank's partials into it->m_local; with fin (single rank) also mean/std/threshold.
-hipError_t launch_merge_moments(const Moments* part, int64_t nparts, IterDev* it, const MomentsFinalize* fin,
-                                hipStream_t s);
+hipError_t launch_merge_moments(const Moments* part, int64_t nparts, const double* dist, int64_t nq, IterDev* it,
+                                const MomentsFinalize* fin, hipStream_t s);
 // Merge `nranks` gathered moments in rank order and compute mean/std/threshold.
 hipError_t launch_finalize_moments(const Moments* gathered, int nranks, IterDev* it, MomentsFinalize fin,
                                    hipStream_t s);
@@ -106,8 +106,9 @@ struct CullLaunch {
 int64_t cull_num_blocks(int64_t n);
 hipError_t launch_cull_cov(const CullLaunch& a, hipStream_t s);
 // Merge the rank's partials into it->c_local; with pub (single rank) also RMSE + publish.
-hipError_t launch_merge_cov(const CovMoments* part, int64_t nparts, IterDev* it, const IterPublish* pub,
-                            hipStream_t s);
+struct CullLaunch;
+hipError_t launch_merge_cov(const CovMoments* part, int64_t nparts, const CullLaunch& cl, IterDev* it,
+                            const IterPublish* pub, hipStream_t s);
 // Merge `nranks` gathered covariance moments in rank order, RMSE, publish.
 hipError_t launch_finalize_cov(const CovMoments* gathered, int nranks, IterDev* it, IterPublish pub, hipStream_t s);
 

@@ -782,53 +782,113 @@ __global__ void __launch_bounds__(256) k_nn_fallback(NNLaunch a) {
   }
 }
 
+// Rank-level reductions as shifted plain sums. A part holds sums of values shifted by a constant
+// of the iteration (query 0's residual, source point and match), so the sums stay at the spread
+// of the data, not at its offset (LAS-sized coordinates), and the merge tree is plain additions
+// in a fixed order: deterministic and cheap.
+// The last level turns them into (count, mean, M2) and (count, means, co-moment) records, which
+// ranks merge with the Chan formulas (icp_common.h).
+struct MomSums {
+  double n, s1, s2, dmin, dmax, nbad, pad0, pad1;  // s1 = sum (d - c), s2 = sum (d - c)^2
+};
+struct CovSums {
+  double n, sum_d2, sa[3], sb[3], sab[9], pad[3];  // sa = sum (a - s), sb = sum (b - t), sab = sum (a - s)(b - t)^T
+};
+static_assert(sizeof(MomSums) == sizeof(Moments) && sizeof(CovSums) == sizeof(CovMoments), "part buffers");
+
+__device__ __forceinline__ MomSums momsum_identity() {
+  MomSums m;
+  m.n = m.s1 = m.s2 = m.nbad = m.pad0 = m.pad1 = 0.0;
+  m.dmin = 1.7976931348623157e308;
+  m.dmax = 0.0;
+  return m;
+}
+__device__ MomSums momsum_merge(const MomSums& a, const MomSums& b) {
+  MomSums r;
+  r.n = a.n + b.n;
+  r.s1 = a.s1 + b.s1;
+  r.s2 = a.s2 + b.s2;
+  r.dmin = b.dmin < a.dmin ? b.dmin : a.dmin;
+  r.dmax = b.dmax > a.dmax ? b.dmax : a.dmax;
+  r.nbad = a.nbad + b.nbad;
+  r.pad0 = r.pad1 = 0.0;
+  return r;
+}
+__device__ __forceinline__ CovSums covsum_identity() {
+  CovSums c;
+  c.n = c.sum_d2 = 0.0;
+  for (int k = 0; k < 3; k++) c.sa[k] = c.sb[k] = c.pad[k] = 0.0;
+  for (int k = 0; k < 9; k++) c.sab[k] = 0.0;
+  return c;
+}
+__device__ CovSums covsum_merge(const CovSums& a, const CovSums& b) {
+  CovSums r;
+  r.n = a.n + b.n;
+  r.sum_d2 = a.sum_d2 + b.sum_d2;
+  for (int k = 0; k < 3; k++) {
+    r.sa[k] = a.sa[k] + b.sa[k];
+    r.sb[k] = a.sb[k] + b.sb[k];
+    r.pad[k] = 0.0;
+  }
+  for (int k = 0; k < 9; k++) r.sab[k] = a.sab[k] + b.sab[k];
+  return r;
+}
+
+// The shifts of this iteration: query 0's residual, its source point and its match (a function of
+// this iteration's data only, so equal inputs give equal bits; every block and the last level
+// compute the same values). Any finite shift is correct; one inside the data keeps the sums at
+// the scale of the data's spread.
+__device__ __forceinline__ double moment_shift(const double* dist, int64_t n) {
+  const double d0 = n > 0 ? dist[0] : 0.0;
+  return __builtin_isfinite(d0) ? d0 : 0.0;
+}
+__device__ __forceinline__ void cov_shift(const double* x, const double* y, const double* z, const int32_t* pos,
+                                          const TgtPt* pts, int64_t n, double sh[6]) {
+  for (int k = 0; k < 6; k++) sh[k] = 0.0;
+  if (n <= 0) return;
+  const TgtPt p = pts[pos[0]];
+  const double v[6] = {x[0], y[0], z[0], p.x, p.y, p.z};
+  for (int k = 0; k < 6; k++) sh[k] = __builtin_isfinite(v[k]) ? v[k] : 0.0;
+}
+
 // Residual moments of the rank's queries in fixed parts of kMomPart queries, once every search
 // kernel has written its residuals: deterministic whatever order the queries were settled in.
-// Thread t of block p holds queries p kMomPart + t + 256 e (e < kMomPer, coalesced); two register
-// passes (mean, then the centered M2, as icpengine.cpp:235-245 computes them over all queries).
+// Thread t of block p holds queries p kMomPart + t + 256 e (e < kMomPer, coalesced).
 constexpr int kMomPer = 16;
 constexpr int kMomPart = 256 * kMomPer;
 
-__global__ void __launch_bounds__(256) k_moments(const double* __restrict__ dist, int64_t n, Moments* part) {
-  __shared__ double red[2 * 4];
+__global__ void __launch_bounds__(256) k_moments(const double* __restrict__ dist, int64_t n, const IterDev* it,
+                                                 MomSums* part) {
+  __shared__ double red[4 * 4];
+  const double c = moment_shift(dist, n);
   const int64_t b0 = (int64_t)blockIdx.x * kMomPart + threadIdx.x;
-  double d[kMomPer];
-  double s1[2] = {0.0, 0.0};
+  double v[4] = {0.0, 0.0, 0.0, 0.0};  // count, sum (d - c), sum (d - c)^2, non-finite
+  double mn = 1.7976931348623157e308, mx = 0.0;
 #pragma unroll
   for (int e = 0; e < kMomPer; e++) {
     const int64_t i = b0 + 256 * e;
     const bool act = i < n;
-    d[e] = act ? dist[i] : 0.0;
-    s1[0] += act ? 1.0 : 0.0;
-    s1[1] += act ? d[e] : 0.0;
+    const double d = act ? dist[i] : 0.0;
+    const double dv = act ? d - c : 0.0;
+    v[0] += act ? 1.0 : 0.0;
+    v[1] += dv;
+    v[2] += dv * dv;
+    const bool fin = act && __builtin_isfinite(d);
+    v[3] += (act && !fin) ? 1.0 : 0.0;
+    mn = fin && d < mn ? d : mn;
+    mx = fin && d > mx ? d : mx;
   }
-  block_sum<2>(s1, red);
-  const double nb = s1[0];
-  const double mean = s1[1] / nb;
-  double s2[2] = {0.0, 0.0};
-  double mn = 1.7976931348623157e308, mx = 0.0;
-#pragma unroll
-  for (int e = 0; e < kMomPer; e++) {
-    const bool act = b0 + 256 * e < n;
-    const double dev = act ? d[e] - mean : 0.0;
-    s2[0] += dev * dev;
-    const bool fin = act && __builtin_isfinite(d[e]);
-    s2[1] += (act && !fin) ? 1.0 : 0.0;
-    mn = fin && d[e] < mn ? d[e] : mn;
-    mx = fin && d[e] > mx ? d[e] : mx;
-  }
-  block_sum<2>(s2, red);
+  block_sum<4>(v, red);
   block_minmax(mn, mx, red);
   if (threadIdx.x == 0) {
-    Moments m;
-    m.n = nb;
-    m.mean = mean;
-    m.m2 = s2[0];
+    MomSums m;
+    m.n = v[0];
+    m.s1 = v[1];
+    m.s2 = v[2];
     m.dmin = mn;
     m.dmax = mx;
-    m.nbad = s2[1];
-    m.pad0 = 0.0;
-    m.pad1 = 0.0;
+    m.nbad = v[3];
+    m.pad0 = m.pad1 = 0.0;
     part[blockIdx.x] = m;
   }
 }
@@ -1906,11 +1966,6 @@ __device__ __forceinline__ T block_tree_last(const T* in, int64_t n, T* sm) {
   return block_tree<T, Merge, Identity>(Merge(q01, q23), sm);
 }
 
-__device__ Moments d_moments_merge(const Moments& a, const Moments& b) { return moments_merge(a, b); }
-__device__ Moments d_moments_identity() { return moments_identity(); }
-__device__ CovMoments d_cov_merge(const CovMoments& a, const CovMoments& b) { return cov_merge(a, b); }
-__device__ CovMoments d_cov_identity() { return cov_identity(); }
-
 template <typename T, T (*Merge)(const T&, const T&), T (*Identity)()>
 __global__ void __launch_bounds__(256) k_tree_merge(const T* in, int64_t n, T* out) {
   __shared__ T sm[256];
@@ -1918,6 +1973,7 @@ __global__ void __launch_bounds__(256) k_tree_merge(const T* in, int64_t n, T* o
   const T r = block_tree<T, Merge, Identity>(g < n ? in[g] : Identity(), sm);
   if (threadIdx.x == 0) out[blockIdx.x] = r;
 }
+
 
 // mean = sum/row; std = sqrt(variance/row) (icpengine.cpp:235-245); threshold rule of the caller
 __device__ void finalize_moments(IterDev* it, const Moments& g, const MomentsFinalize& f) {
@@ -1929,14 +1985,26 @@ __device__ void finalize_moments(IterDev* it, const Moments& g, const MomentsFin
   it->thr = cull_threshold(mean, sd, f.k_sigma, f.iter, f.engine_rules);
 }
 
-// Last level of the rank's moments merge: it->m_local; with fin (one rank) also the statistics.
-__global__ void __launch_bounds__(256) k_merge_moments_last(const Moments* in, int64_t n, IterDev* it,
-                                                           MomentsFinalize fin, int finalize) {
-  __shared__ Moments sm[256];
-  const Moments r = block_tree_last<Moments, d_moments_merge, d_moments_identity>(in, n, sm);
+// Last level of the rank's moments: the summed part -> (count, mean, M2) in it->m_local; with fin
+// (one rank) also the statistics.
+__global__ void __launch_bounds__(256) k_merge_moments_last(const MomSums* in, int64_t n, const double* dist,
+                                                           int64_t nq, IterDev* it, MomentsFinalize fin, int finalize) {
+  __shared__ MomSums sm[256];
+  const MomSums r = block_tree_last<MomSums, momsum_merge, momsum_identity>(in, n, sm);
   if (threadIdx.x == 0) {
-    it->m_local = r;
-    if (finalize) finalize_moments(it, r, fin);
+    const double c = moment_shift(dist, nq);
+    Moments m = moments_identity();
+    if (r.n > 0.0) {
+      m.n = r.n;
+      m.mean = c + r.s1 / r.n;
+      const double m2 = r.s2 - r.s1 * (r.s1 / r.n);
+      m.m2 = m2 < 0.0 ? 0.0 : m2;  // rounding only; NaN propagates
+      m.dmin = r.dmin;
+      m.dmax = r.dmax;
+    }
+    m.nbad = r.nbad;
+    it->m_local = m;
+    if (finalize) finalize_moments(it, m, fin);
   }
 }
 
@@ -1977,17 +2045,35 @@ __device__ void finalize_cov_publish(IterDev* it, const CovMoments& g, IterPubli
   }
 }
 
-__global__ void __launch_bounds__(256) k_merge_cov_last(const CovMoments* in, int64_t n, IterDev* it, IterPublish pub,
-                                                       int finalize) {
-  __shared__ CovMoments sm[256];
+__global__ void __launch_bounds__(256) k_merge_cov_last(const CovSums* in, int64_t n, CullLaunch cl, IterDev* it,
+                                                       IterPublish pub, int finalize) {
+  __shared__ CovSums sm[256];
   __shared__ IterDev rec;
-  const CovMoments r = block_tree_last<CovMoments, d_cov_merge, d_cov_identity>(in, n, sm);
-  if (!finalize) {
-    if (threadIdx.x == 0) it->c_local = r;
-    return;
+  const CovSums r = block_tree_last<CovSums, covsum_merge, covsum_identity>(in, n, sm);
+  __shared__ CovMoments res;
+  if (threadIdx.x == 0) {
+    double sh[6];
+    cov_shift(cl.x, cl.y, cl.z, cl.pos, cl.pts, cl.n, sh);
+    CovMoments m = cov_identity();
+    if (r.n > 0.0) {
+      m.n = r.n;
+      m.sum_d2 = r.sum_d2;
+      double da[3], db[3];
+      for (int k = 0; k < 3; k++) {
+        da[k] = r.sa[k] / r.n;
+        db[k] = r.sb[k] / r.n;
+        m.ma[k] = sh[k] + da[k];
+        m.mb[k] = sh[3 + k] + db[k];
+      }
+      for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) m.c[3 * i + j] = r.sab[3 * i + j] - r.n * (da[i] * db[j]);
+    }
+    it->c_local = m;
+    res = m;
   }
-  if (threadIdx.x == 0) it->c_local = r;
-  finalize_cov_publish(it, r, pub, &rec);
+  if (!finalize) return;
+  __syncthreads();
+  finalize_cov_publish(it, res, pub, &rec);
 }
 
 __global__ void __launch_bounds__(64) k_finalize_cov(const CovMoments* gathered, int nranks, IterDev* it,
@@ -2001,78 +2087,50 @@ __global__ void __launch_bounds__(64) k_finalize_cov(const CovMoments* gathered,
 constexpr int kCullPer = 4;  // queries per thread of k_cull_cov
 
 __global__ void __launch_bounds__(256) k_cull_cov(CullLaunch a) {
-  __shared__ double red[4 * 9];
+  __shared__ double red[4 * 17];
   const double thr = a.it->thr;
+  double sh[6];
+  cov_shift(a.x, a.y, a.z, a.pos, a.pts, a.n, sh);
   const int64_t blk = xcd_block(a.xcd_remap);
   const int64_t base = blk * (256 * kCullPer) + threadIdx.x;
-  bool valid[kCullPer];
-  double d[kCullPer], ax[kCullPer], ay[kCullPer], az[kCullPer], bx[kCullPer], by[kCullPer], bz[kCullPer];
+  // count, sum d^2, sum (a - s), sum (b - t), sum (a - s)(b - t)^T over the valid pairs
+  double v[17];
+#pragma unroll
+  for (int k = 0; k < 17; k++) v[k] = 0.0;
 #pragma unroll
   for (int e = 0; e < kCullPer; e++) {
     const int64_t i = base + e * 256;
-    valid[e] = false;
-    d[e] = ax[e] = ay[e] = az[e] = bx[e] = by[e] = bz[e] = 0.0;
     if (i < a.n) {
-      d[e] = a.dist[i];
-      valid[e] = d[e] <= thr;  // icpengine.cpp:265
-      if (valid[e]) {
-        ax[e] = a.x[i];
-        ay[e] = a.y[i];
-        az[e] = a.z[i];
+      const double d = a.dist[i];
+      if (d <= thr) {  // icpengine.cpp:265
         const TgtPt* p = a.pts + a.pos[i];
         const double2 pxy = *reinterpret_cast<const double2*>(&p->x);
-        bx[e] = pxy.x;
-        by[e] = pxy.y;
-        bz[e] = p->z;
+        const double da[3] = {a.x[i] - sh[0], a.y[i] - sh[1], a.z[i] - sh[2]};
+        const double db[3] = {pxy.x - sh[3], pxy.y - sh[4], p->z - sh[5]};
+        v[0] += 1.0;
+        v[1] += d * d;
+#pragma unroll
+        for (int r = 0; r < 3; r++) {
+          v[2 + r] += da[r];
+          v[5 + r] += db[r];
+#pragma unroll
+          for (int c = 0; c < 3; c++) v[8 + 3 * r + c] += da[r] * db[c];
+        }
       }
     }
   }
-  double s1[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-#pragma unroll
-  for (int e = 0; e < kCullPer; e++) {
-    s1[0] += valid[e] ? 1.0 : 0.0;
-    s1[1] += valid[e] ? d[e] * d[e] : 0.0;
-    s1[2] += ax[e];
-    s1[3] += ay[e];
-    s1[4] += az[e];
-    s1[5] += bx[e];
-    s1[6] += by[e];
-    s1[7] += bz[e];
-  }
-  block_sum<8>(s1, red);
-  const double nb = s1[0];
-  if (nb == 0.0) {
-    if (threadIdx.x == 0) a.part[blk] = cov_identity();
-    return;
-  }
-  const double ma[3] = {s1[2] / nb, s1[3] / nb, s1[4] / nb};
-  const double mb[3] = {s1[5] / nb, s1[6] / nb, s1[7] / nb};
-  double s2[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-#pragma unroll
-  for (int e = 0; e < kCullPer; e++) {
-    const double ca[3] = {valid[e] ? ax[e] - ma[0] : 0.0, valid[e] ? ay[e] - ma[1] : 0.0,
-                          valid[e] ? az[e] - ma[2] : 0.0};
-    const double cb[3] = {valid[e] ? bx[e] - mb[0] : 0.0, valid[e] ? by[e] - mb[1] : 0.0,
-                          valid[e] ? bz[e] - mb[2] : 0.0};
-#pragma unroll
-    for (int r = 0; r < 3; r++)
-#pragma unroll
-      for (int c = 0; c < 3; c++) s2[3 * r + c] += ca[r] * cb[c];
-  }
-  block_sum<9>(s2, red);
+  block_sum<17>(v, red);
   if (threadIdx.x == 0) {
-    CovMoments m;
-    m.n = nb;
-    m.sum_d2 = s1[1];
+    CovSums m;
+    m.n = v[0];
+    m.sum_d2 = v[1];
     for (int k = 0; k < 3; k++) {
-      m.ma[k] = ma[k];
-      m.mb[k] = mb[k];
+      m.sa[k] = v[2 + k];
+      m.sb[k] = v[5 + k];
+      m.pad[k] = 0.0;
     }
-    for (int k = 0; k < 9; k++) m.c[k] = s2[k];
-    m.pad[0] = 0.0;
-    m.pad[1] = 0.0;
-    m.pad[2] = 0.0;
-    a.part[blk] = m;
+    for (int k = 0; k < 9; k++) m.sab[k] = v[8 + k];
+    reinterpret_cast<CovSums*>(a.part)[blk] = m;
   }
 }
 
@@ -2283,18 +2341,20 @@ static const T* merge_to_last_span(const T* part, int64_t* nparts, hipStream_t s
   return cur;
 }
 
-hipError_t launch_merge_moments(const Moments* part, int64_t nparts, IterDev* it, const MomentsFinalize* fin,
-                                hipStream_t s) {
-  const Moments* cur = merge_to_last_span<Moments, d_moments_merge, d_moments_identity>(part, &nparts, s);
-  hipLaunchKernelGGL(k_merge_moments_last, dim3(1), dim3(256), 0, s, cur, nparts, it,
+hipError_t launch_merge_moments(const Moments* part, int64_t nparts, const double* dist, int64_t nq, IterDev* it,
+                                const MomentsFinalize* fin, hipStream_t s) {
+  const MomSums* cur = merge_to_last_span<MomSums, momsum_merge, momsum_identity>(
+      reinterpret_cast<const MomSums*>(part), &nparts, s);
+  hipLaunchKernelGGL(k_merge_moments_last, dim3(1), dim3(256), 0, s, cur, nparts, dist, nq, it,
                      fin ? *fin : MomentsFinalize{0.0, 0, 0}, fin ? 1 : 0);
   return hipGetLastError();
 }
 
-hipError_t launch_merge_cov(const CovMoments* part, int64_t nparts, IterDev* it, const IterPublish* pub,
-                            hipStream_t s) {
-  const CovMoments* cur = merge_to_last_span<CovMoments, d_cov_merge, d_cov_identity>(part, &nparts, s);
-  hipLaunchKernelGGL(k_merge_cov_last, dim3(1), dim3(256), 0, s, cur, nparts, it,
+hipError_t launch_merge_cov(const CovMoments* part, int64_t nparts, const CullLaunch& cl, IterDev* it,
+                            const IterPublish* pub, hipStream_t s) {
+  const CovSums* cur = merge_to_last_span<CovSums, covsum_merge, covsum_identity>(
+      reinterpret_cast<const CovSums*>(part), &nparts, s);
+  hipLaunchKernelGGL(k_merge_cov_last, dim3(1), dim3(256), 0, s, cur, nparts, cl, it,
                      pub ? *pub : IterPublish{nullptr, nullptr, 0.0}, pub ? 1 : 0);
   return hipGetLastError();
 }
@@ -2307,9 +2367,10 @@ hipError_t launch_finalize_moments(const Moments* gathered, int nranks, IterDev*
 
 int64_t moments_num_parts(int64_t n) { return (n + kMomPart - 1) / kMomPart; }
 
-hipError_t launch_moments(const double* dist, int64_t n, Moments* part, hipStream_t s) {
+hipError_t launch_moments(const double* dist, int64_t n, const IterDev* it, Moments* part, hipStream_t s) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_moments, dim3((unsigned)moments_num_parts(n)), dim3(256), 0, s, dist, n, part);
+  hipLaunchKernelGGL(k_moments, dim3((unsigned)moments_num_parts(n)), dim3(256), 0, s, dist, n, it,
+                     reinterpret_cast<MomSums*>(part));
   return hipGetLastError();
 }
 
