@@ -1929,10 +1929,11 @@ __global__ void __launch_bounds__(64) k_nn_lists(NNLaunch a) {
   }
 }
 
-// Fixed-shape merges of block partials (Chan et al. pairwise formulas), deterministic: the same
+// Fixed-shape merges of block partials (plain sums; Moments/CovMoments keep the Chan formulas for
+// the rank merge), deterministic: the same
 // n always gives the same merge tree. Inner levels: block b merges items [256 b, 256 b + 256),
-// one per thread, pairwise in LDS. Last level: one block, up to 4096 items, thread t merges its
-// 16 consecutive items pairwise (quads, then quads of quads), then the block's pairwise tree.
+// one per thread, pairwise in LDS. Last level: one block, up to 4096 items: thread t folds items
+// t + 256 k (k < 16) in order, then the block's pairwise tree.
 constexpr int kLastSpan = 4096;
 
 template <typename T, T (*Merge)(const T&, const T&), T (*Identity)()>
@@ -1948,22 +1949,17 @@ __device__ __forceinline__ T block_tree(T v, T* sm) {
 }
 
 template <typename T, T (*Merge)(const T&, const T&), T (*Identity)()>
-__device__ __forceinline__ T block_quad(const T* in, int64_t n, int64_t g) {
-  const T i0 = g < n ? in[g] : Identity();
-  const T i1 = g + 1 < n ? in[g + 1] : Identity();
-  const T i2 = g + 2 < n ? in[g + 2] : Identity();
-  const T i3 = g + 3 < n ? in[g + 3] : Identity();
-  return Merge(Merge(i0, i1), Merge(i2, i3));
-}
-
-template <typename T, T (*Merge)(const T&, const T&), T (*Identity)()>
 __device__ __forceinline__ T block_tree_last(const T* in, int64_t n, T* sm) {
-  // thread t: items 16t .. 16t + 15 as ((q0, q1), (q2, q3)) of quads ((0, 1), (2, 3))
-  // (no early exit: block_tree's barriers must be reached by every thread in uniform control flow)
-  const int64_t g = 16 * (int64_t)threadIdx.x;
-  const T q01 = Merge(block_quad<T, Merge, Identity>(in, n, g), block_quad<T, Merge, Identity>(in, n, g + 4));
-  const T q23 = Merge(block_quad<T, Merge, Identity>(in, n, g + 8), block_quad<T, Merge, Identity>(in, n, g + 12));
-  return block_tree<T, Merge, Identity>(Merge(q01, q23), sm);
+  // thread t folds items t, t + 256, ..., t + 15 * 256 in that order (coalesced across the block;
+  // the merges of the partial sums are additions, cheap in a chain), then the block's tree.
+  // No early exit: block_tree's barriers must be reached by every thread in uniform control flow.
+  T acc = Identity();
+#pragma unroll 4
+  for (int k = 0; k < 16; k++) {
+    const int64_t g = (int64_t)threadIdx.x + 256 * k;
+    if (g < n) acc = Merge(acc, in[g]);
+  }
+  return block_tree<T, Merge, Identity>(acc, sm);
 }
 
 template <typename T, T (*Merge)(const T&, const T&), T (*Identity)()>
@@ -2020,8 +2016,13 @@ __global__ void k_finalize_moments(const Moments* gathered, int nranks, IterDev*
 // stream synchronisation that follows makes it visible. The list sizes ride along (pad[0..2])
 // and are reset for the next search.
 __device__ void finalize_cov_publish(IterDev* it, const CovMoments& g, IterPublish pub, IterDev* rec) {
+  constexpr int kWords = (int)(sizeof(IterDev) / sizeof(double)) - 1;  // all but pad[3], the flag
+  static_assert(offsetof(IterDev, pad) + 3 * sizeof(double) == kWords * sizeof(double), "flag is the last word");
+  double* rw = reinterpret_cast<double*>(rec);
+  const double* iw = reinterpret_cast<const double*>(it);
+  for (int k = threadIdx.x; k < kWords + 1; k += blockDim.x) rw[k] = iw[k];  // the device record, in parallel
+  __syncthreads();
   if (threadIdx.x == 0) {
-    *rec = *it;
     rec->c_global = g;
     rec->rmse = (g.n > 0) ? __builtin_sqrt(g.sum_d2 / g.n) : 0.0;  // icpengine.cpp:274-278
     for (int k = 0; k < 3; k++) {
@@ -2032,17 +2033,15 @@ __device__ void finalize_cov_publish(IterDev* it, const CovMoments& g, IterPubli
     it->rmse = rec->rmse;
   }
   __syncthreads();
-  const double* src = reinterpret_cast<const double*>(rec);
+  // System-scope stores straight to the host page (no L2 write-back of the whole cache, which a
+  // system-scope release fence would do: the search just dirtied megabytes of it); each thread
+  // waits for its stores to be acknowledged before the block's sequence word goes out.
   double* dst = reinterpret_cast<double*>(pub.host);
-  constexpr int kWords = (int)(sizeof(IterDev) / sizeof(double)) - 1;  // all but pad[3], the flag
-  static_assert(offsetof(IterDev, pad) + 3 * sizeof(double) == kWords * sizeof(double), "flag is the last word");
-  for (int k = threadIdx.x; k < kWords; k += blockDim.x) dst[k] = src[k];
-  __threadfence_system();
+  for (int k = threadIdx.x; k < kWords; k += blockDim.x)
+    __hip_atomic_store(dst + k, rw[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
-  if (threadIdx.x == 0) {
-    *reinterpret_cast<volatile double*>(&pub.host->pad[3]) = pub.seq;
-    __threadfence_system();
-  }
+  if (threadIdx.x == 0) __hip_atomic_store(&pub.host->pad[3], pub.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 __global__ void __launch_bounds__(256) k_merge_cov_last(const CovSums* in, int64_t n, CullLaunch cl, IterDev* it,
