@@ -286,3 +286,28 @@ def test_scan32_ties_and_self_queries(icp, oracle, golden_nn):
         oidx, od = oracle.OracleTree(t).nn(q, init_best=1e20)
         np.testing.assert_array_equal(idx, oidx)
         np.testing.assert_array_equal(d, od)
+
+
+def test_session_step_n_equals_steps(icp):
+    """icp_session_step_n (the bench's timed loop) is the same loop as repeated icp_session_step:
+    identical transforms bit for bit; it stops at convergence like the step loop."""
+    tgt, src, _ = icp.synth_pair(200_000, yaw_deg=4.0)
+
+    def run(native: bool):
+        with icp.Context(0) as ctx:
+            ctx.set_target(tgt, 10, 20, icp.RULES_ENGINE)
+            ctx.set_source(src)
+            sess = ctx.session(icp.params_default(max_iterations=40, tolerance=1e-9))
+            if native:
+                taken = sess.step_n(1000)
+            else:
+                taken = 0
+                while not sess.done:
+                    sess.step()
+                    taken += 1
+            return taken, sess.transform().copy()
+
+    na, Ta = run(True)
+    nb, Tb = run(False)
+    assert na == nb and 0 < na <= 40
+    assert np.array_equal(Ta, Tb)
