@@ -115,6 +115,7 @@ int icp_hip_create(icp_hip_ctx** out, int device) {
   if (const char* v = std::getenv("ICP_CELLS")) c->use_cells = std::atoi(v);
   if (const char* v = std::getenv("ICP_XCD")) c->xcd_remap = std::atoi(v);
   if (const char* v = std::getenv("ICP_BALL_GROUPS")) c->ball_groups = std::atoi(v);
+  if (const char* v = std::getenv("ICP_JOIN")) c->join_factor = std::atof(v);
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
     delete c;
     return fail(ICP_HIP_EDEVICE, "hipStreamCreate failed");
@@ -384,6 +385,7 @@ int icp_hip_iterate(icp_hip_ctx* c, const double* T_apply, int iter, int rules, 
   a.cell_lmax = c->cell_lmax;
   a.xcd_remap = c->xcd_remap;
   a.ball_groups = c->ball_groups;
+  a.join_factor = c->join_factor;
   for (int k = 0; k < 3; k++) {
     a.root_lo[k] = c->root_box[k];
     a.root_hi[k] = c->root_box[3 + k];
@@ -587,6 +589,7 @@ int icp_hip_nn(icp_hip_ctx* c, const double* q, int64_t n, int32_t* idx_out, dou
   a.cell_lmax = c->cell_lmax;
   a.xcd_remap = c->xcd_remap;
   a.ball_groups = c->ball_groups;
+  a.join_factor = c->join_factor;
   for (int k = 0; k < 3; k++) {
     a.root_lo[k] = c->root_box[k];
     a.root_hi[k] = c->root_box[3 + k];
@@ -648,6 +651,7 @@ int icp_hip_traversal_counts(icp_hip_ctx* c, double* mean_entries, double* mean_
   a.cell_lmax = c->cell_lmax;
   a.xcd_remap = c->xcd_remap;
   a.ball_groups = c->ball_groups;
+  a.join_factor = c->join_factor;
   for (int k = 0; k < 3; k++) {
     a.root_lo[k] = c->root_box[k];
     a.root_hi[k] = c->root_box[3 + k];

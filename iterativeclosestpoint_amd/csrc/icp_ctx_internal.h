@@ -16,6 +16,7 @@ struct icp_hip_ctx {
   int scan32 = 1;         // fp32 filter scan in the wave search (ICP_SCAN32=0: fp64 scan)
   int lca_descent = 1;    // uniform descent before the wave's breadth-first walk (ICP_LCA=0: off)
   int use_cells = 1;      // start the wave walk from the cell tables (ICP_CELLS=0: off)
+  double join_factor = 3.0;  // wave-box join rule: radius <= factor x the wave's mean (ICP_JOIN)
   int ball_groups = 4;    // queries per wave of the ball search (ICP_BALL_GROUPS=1: one)
   int xcd_remap = 0;      // XCD-contiguous block order for search and cull (ICP_XCD=1; measured: no gain)
   hipStream_t stream = nullptr;

@@ -58,6 +58,7 @@ struct NNLaunch {
   unsigned long long* dbg; // optional diagnostics of the wave-cooperative search (ICP_NN_DEBUG)
   int xcd_remap;           // variant 4: each XCD takes one contiguous range of query blocks
   int ball_groups;         // variant 4: queries per wave of the ball search (4; 1 = one per wave)
+  double join_factor;      // variant 4: a lane joins the wave box if its radius <= this x the mean radius
 };
 
 // Threads per block of the NN kernel for a given stack depth.

@@ -898,8 +898,8 @@ __global__ void __launch_bounds__(256) k_moments(const double* __restrict__ dist
 //
 // The 64 queries of a wave are Morton neighbours. Each lane first descends (nearest child, no
 // backtracking) to a leaf and scans it: u = an actual point's fl(d2), an upper bound of its
-// nearest distance. Lanes whose radius r = sqrt(u)(1 + 2^-40) + |q| 2^-45 is below twice the
-// wave's mean radius join one search box B = bbox of [q - r, q + r]; the wave collects every leaf
+// nearest distance. Lanes whose radius r = sqrt(u)(1 + 2^-40) + |q| 2^-45 is at most 3x the
+// wave's mean radius (NNLaunch::join_factor, ICP_JOIN) join one search box B = bbox of [q - r, q + r]; the wave collects every leaf
 // whose box meets B by a cooperative breadth-first walk (frontier and leaf list in LDS), then
 // all lanes scan those points in lockstep (wave-uniform loop, uniform addresses). Each joined
 // lane's ball of radius r lies in B, so every point with fl(d2) <= best (1 + 2^-48) is among
@@ -1106,7 +1106,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
   const double r = cand ? __builtin_sqrt(u) * (1.0 + 0x1p-40) + amax * 0x1p-45 : 0.0;
   const unsigned long long cmask = __ballot(cand);
   const double mean_r = wave_sum_d(r) / (double)(cmask ? __popcll(cmask) : 1);
-  bool join = cand && r <= 2.0 * mean_r;
+  bool join = cand && r <= a.join_factor * mean_r;
   const double blx = wave_min_d(join ? qx - r : __builtin_inf());
   const double bly = wave_min_d(join ? qy - r : __builtin_inf());
   const double blz = wave_min_d(join ? qz - r : __builtin_inf());
