@@ -104,6 +104,9 @@ def main() -> int:
     ap.add_argument("--points", type=int, default=10_000_000, help="points per cloud (config 4: 10M)")
     ap.add_argument("--cpu-sample", type=int, default=1_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--exchange", choices=("rccl", "host"), default="rccl",
+                    help="per-iteration all-gathers: RCCL (default), or over torch.distributed gloo "
+                         "through the host (rehearsal of N ranks on one GPU; RCCL refuses that)")
     ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "traffic_latest.json"),
                     help="PMC-derived HBM bytes per search launch (written by tools/pmc_traffic.py)")
     args = ap.parse_args()
@@ -130,7 +133,14 @@ def main() -> int:
     # spatial shards: contiguous ranges of the kd order (a contiguous range of the shuffled cloud
     # would thin each rank's queries `world` times; see icp_host.h icp_source_shard_order)
     ctx.set_source(src[icp.source_shard_order(src)[lo:hi]] if world > 1 else src)
-    if world > 1:
+    if world > 1 and args.exchange == "host":
+        def exchange(local):
+            t = torch.from_numpy(local)
+            out = [torch.zeros_like(t) for _ in range(world)]
+            dist.all_gather(out, t)
+            return torch.stack(out).numpy()
+        ctx.comm_init_host(world, rank, exchange)
+    elif world > 1:
         uid = [icp.Context.unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         ctx.comm_init(world, rank, uid[0])
@@ -213,7 +223,7 @@ def main() -> int:
                             f"(engine rules, octree leaf 10 / depth 20), "
                             f"source sharded over {world} GPU(s), target octree replicated",
                 "n_target": n, "n_source": n, "parallelism": f"spatial source shards x{world} (kd-order ranges; "
-                "RCCL all-gather of 2 moment records per iteration)",
+                + ("RCCL" if args.exchange == "rccl" else "host/gloo") + " all-gather of 2 moment records per iteration)",
                 "octree_nodes": info["n_nodes"], "octree_leaves": info["n_leaves"],
             },
             "roofline": {

@@ -80,6 +80,15 @@ void icp_hip_destroy(icp_hip_ctx* ctx);
 int icp_hip_get_unique_id(uint8_t out[ICP_HIP_UNIQUE_ID_BYTES]);
 int icp_hip_comm_init(icp_hip_ctx* ctx, int nranks, int rank, const uint8_t id[ICP_HIP_UNIQUE_ID_BYTES]);
 
+/* Multi-rank without RCCL: the two per-iteration all-gathers go through the caller's callback.
+ * `exchange` receives this rank's record (`count` doubles) and fills `gathered` with every
+ * rank's record in rank order (nranks x count); it returns 0 on success. The rest of the
+ * multi-rank path (rank-order merge on the device, publish) is the one comm_init runs. Used to
+ * rehearse several ranks on one GPU (RCCL refuses two ranks on one device) and by callers that
+ * already own a host transport. Slower than RCCL: the stream is synchronised around each call. */
+typedef int (*icp_hip_exchange_fn)(void* user, const double* local, int32_t count, double* gathered);
+int icp_hip_comm_init_host(icp_hip_ctx* ctx, int nranks, int rank, icp_hip_exchange_fn exchange, void* user);
+
 /* Build the reference octree of the target (AoS xyz, n points) and keep it in HBM. The tree is
  * built on the device (max_depth <= 21; env ICP_OCTREE_BUILD=host forces the host builder) or on
  * the host (deeper trees); both produce the same arrays bit for bit. rules selects the initial

@@ -104,6 +104,8 @@ class SynthSpec(C.Structure):
     ]
 
 
+_EXCHANGE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_double), C.c_int32, C.POINTER(C.c_double))
+
 # (name, restype, argtypes) for every exported symbol; also the list the ABI test checks
 SIGNATURES = {
     # icp_hip.h
@@ -112,6 +114,7 @@ SIGNATURES = {
     "icp_hip_destroy": (None, [_P]),
     "icp_hip_get_unique_id": (C.c_int, [C.c_char_p]),
     "icp_hip_comm_init": (C.c_int, [_P, C.c_int, C.c_int, C.c_char_p]),
+    "icp_hip_comm_init_host": (C.c_int, [_P, C.c_int, C.c_int, C.c_void_p, _P]),
     "icp_hip_set_target": (C.c_int, [_P, _P, C.c_int64, C.c_int, C.c_int, C.c_int]),
     "icp_hip_set_source": (C.c_int, [_P, _P, C.c_int64]),
     "icp_hip_iterate": (C.c_int, [_P, _P, C.c_int, C.c_int, C.c_double, C.POINTER(IterStats)]),
@@ -261,6 +264,22 @@ class Context:
 
     def comm_init(self, nranks: int, rank: int, uid: bytes):
         _check(lib().icp_hip_comm_init(self._h, nranks, rank, C.c_char_p(bytes(uid))))
+
+    def comm_init_host(self, nranks: int, rank: int, exchange):
+        """Multi-rank with the all-gathers done by `exchange(local) -> (nranks, count) array`
+        (rank order) instead of RCCL (icp_hip_comm_init_host): rehearses several ranks on one GPU."""
+        def _cb(_user, local, count, gathered):
+            try:
+                loc = np.ctypeslib.as_array(local, shape=(count,)).copy()
+                out = np.ascontiguousarray(exchange(loc), dtype=np.float64).reshape(-1)
+                if out.shape[0] != nranks * count:
+                    return 1
+                C.memmove(gathered, out.ctypes.data, out.nbytes)
+                return 0
+            except Exception:
+                return 1
+        self._xcb = _EXCHANGE_FN(_cb)  # kept alive as long as the context
+        _check(lib().icp_hip_comm_init_host(self._h, nranks, rank, C.cast(self._xcb, C.c_void_p), None))
 
     def set_target(self, xyz, max_points=10, max_depth=20, rules=RULES_ENGINE):
         xyz = _aos(xyz)

@@ -192,6 +192,42 @@ int icp_hip_comm_init(icp_hip_ctx* c, int nranks, int rank, const uint8_t id_byt
   return ICP_HIP_OK;
 }
 
+int icp_hip_comm_init_host(icp_hip_ctx* c, int nranks, int rank, icp_hip_exchange_fn exchange, void* user) {
+  if (!c || nranks < 1 || rank < 0 || rank >= nranks || (nranks > 1 && !exchange))
+    return fail(ICP_HIP_EINVAL, "bad comm arguments");
+  HIP_TRY(hipSetDevice(c->device));
+  if (c->comm) {
+    (void)ncclCommDestroy(c->comm);
+    c->comm = nullptr;
+  }
+  c->nranks = nranks;
+  c->rank = rank;
+  c->xfn = nranks > 1 ? exchange : nullptr;
+  c->xuser = user;
+  if (nranks == 1) return ICP_HIP_OK;
+  dfree(c->gm);
+  dfree(c->gc);
+  HIP_TRY(dalloc(&c->gm, (size_t)nranks));
+  HIP_TRY(dalloc(&c->gc, (size_t)nranks));
+  return ICP_HIP_OK;
+}
+
+// The per-iteration all-gather of one record (count doubles) in rank order: RCCL on the compute
+// stream, or the caller's host exchange (stream synchronised around the callback).
+static int all_gather_record(icp_hip_ctx* c, const double* d_local, double* d_gathered, int count, hipStream_t s) {
+  if (c->comm) {
+    RCCL_TRY(ncclAllGather(d_local, d_gathered, (size_t)count, ncclDouble, c->comm, s));
+    return ICP_HIP_OK;
+  }
+  std::vector<double> local((size_t)count), all((size_t)count * c->nranks);
+  HIP_TRY(hipMemcpyAsync(local.data(), d_local, sizeof(double) * count, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  if (c->xfn(c->xuser, local.data(), count, all.data()) != 0) return fail(ICP_HIP_ERCCL, "host exchange callback failed");
+  HIP_TRY(hipMemcpyAsync(d_gathered, all.data(), sizeof(double) * all.size(), hipMemcpyHostToDevice, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  return ICP_HIP_OK;
+}
+
 int icp_hip_set_target(icp_hip_ctx* c, const double* xyz, int64_t n, int max_points, int max_depth, int rules) {
   if (!c || (!xyz && n > 0)) return fail(ICP_HIP_EINVAL, "null argument");
   if (n <= 0) return fail(ICP_HIP_EINVAL, "empty target cloud (icpengine.cpp:31-34 rejects it)");
@@ -355,7 +391,7 @@ int icp_hip_iterate(icp_hip_ctx* c, const double* T_apply, int iter, int rules, 
   if (!c || !out) return fail(ICP_HIP_EINVAL, "null argument");
   if (!c->nodes) return fail(ICP_HIP_ENOTREADY, "target not set");
   if (!c->x && c->n_src > 0) return fail(ICP_HIP_ENOTREADY, "source not set");
-  if (c->nranks > 1 && !c->comm) return fail(ICP_HIP_ENOTREADY, "communicator not initialised");
+  if (c->nranks > 1 && !c->comm && !c->xfn) return fail(ICP_HIP_ENOTREADY, "communicator not initialised");
   HIP_TRY(hipSetDevice(c->device));
   hipStream_t s = c->stream;
   hipEvent_t* ev = c->ring[c->n_iterates % icp_hip_ctx::kTimingRing];
@@ -416,7 +452,9 @@ int icp_hip_iterate(icp_hip_ctx* c, const double* T_apply, int iter, int rules, 
   HIP_TRY(launch_moments(c->dist, c->n_src, c->it, c->mparts, s));
   HIP_TRY(launch_merge_moments(c->mparts, c->nb_mom, c->dist, c->n_src, c->it, multi ? nullptr : &fin, s));
   if (multi) {
-    RCCL_TRY(ncclAllGather(&c->it->m_local, c->gm, sizeof(Moments) / sizeof(double), ncclDouble, c->comm, s));
+    const int rc = all_gather_record(c, reinterpret_cast<const double*>(&c->it->m_local),
+                                     reinterpret_cast<double*>(c->gm), (int)(sizeof(Moments) / sizeof(double)), s);
+    if (rc != ICP_HIP_OK) return rc;
     HIP_TRY(launch_finalize_moments(c->gm, c->nranks, c->it, fin, s));
   }
   CullLaunch cl;
@@ -436,7 +474,9 @@ int icp_hip_iterate(icp_hip_ctx* c, const double* T_apply, int iter, int rules, 
   const IterPublish pub{c->h_it_dev, c->fb_count, (double)seq};
   HIP_TRY(launch_merge_cov(c->cparts, c->nb_cull, cl, c->it, multi ? nullptr : &pub, s));
   if (multi) {
-    RCCL_TRY(ncclAllGather(&c->it->c_local, c->gc, sizeof(CovMoments) / sizeof(double), ncclDouble, c->comm, s));
+    const int rc = all_gather_record(c, reinterpret_cast<const double*>(&c->it->c_local),
+                                     reinterpret_cast<double*>(c->gc), (int)(sizeof(CovMoments) / sizeof(double)), s);
+    if (rc != ICP_HIP_OK) return rc;
     HIP_TRY(launch_finalize_cov(c->gc, c->nranks, c->it, pub, s));
   }
   HIP_TRY(hipEventRecord(ev[3], s));

@@ -6,6 +6,7 @@
 
 #include <cstdint>
 
+#include "../../include/icp_hip.h"
 #include "kernels.h"
 
 struct icp_hip_ctx {
@@ -68,6 +69,8 @@ struct icp_hip_ctx {
   // multi-GPU
   int nranks = 1, rank = 0;
   ncclComm_t comm = nullptr;
+  icp_hip_exchange_fn xfn = nullptr;  // host exchange instead of RCCL (icp_hip_comm_init_host)
+  void* xuser = nullptr;
   icp::Moments* gm = nullptr;
   icp::CovMoments* gc = nullptr;
 };

@@ -2096,16 +2096,36 @@ __global__ void __launch_bounds__(256) k_cull_cov(CullLaunch a) {
   double v[17];
 #pragma unroll
   for (int k = 0; k < 17; k++) v[k] = 0.0;
+  // All streamed loads first, then all match gathers (a culled or missing query gathers point 0,
+  // always valid): two dependent memory round trips per thread instead of three.
+  double dq[kCullPer], qx[kCullPer], qy[kCullPer], qz[kCullPer];
+  int32_t pq[kCullPer];
 #pragma unroll
   for (int e = 0; e < kCullPer; e++) {
     const int64_t i = base + e * 256;
-    if (i < a.n) {
-      const double d = a.dist[i];
+    const bool in = i < a.n;
+    dq[e] = in ? a.dist[i] : __builtin_nan("");  // NaN <= thr is false: not a valid pair
+    pq[e] = in ? a.pos[i] : 0;
+    qx[e] = in ? a.x[i] : 0.0;
+    qy[e] = in ? a.y[i] : 0.0;
+    qz[e] = in ? a.z[i] : 0.0;
+  }
+  double mx[kCullPer], my[kCullPer], mz[kCullPer];
+#pragma unroll
+  for (int e = 0; e < kCullPer; e++) {
+    const TgtPt* p = a.pts + (dq[e] <= thr ? pq[e] : 0);
+    const double2 pxy = *reinterpret_cast<const double2*>(&p->x);
+    mx[e] = pxy.x;
+    my[e] = pxy.y;
+    mz[e] = p->z;
+  }
+#pragma unroll
+  for (int e = 0; e < kCullPer; e++) {
+    {
+      const double d = dq[e];
       if (d <= thr) {  // icpengine.cpp:265
-        const TgtPt* p = a.pts + a.pos[i];
-        const double2 pxy = *reinterpret_cast<const double2*>(&p->x);
-        const double da[3] = {a.x[i] - sh[0], a.y[i] - sh[1], a.z[i] - sh[2]};
-        const double db[3] = {pxy.x - sh[3], pxy.y - sh[4], p->z - sh[5]};
+        const double da[3] = {qx[e] - sh[0], qy[e] - sh[1], qz[e] - sh[2]};
+        const double db[3] = {mx[e] - sh[3], my[e] - sh[4], mz[e] - sh[5]};
         v[0] += 1.0;
         v[1] += d * d;
 #pragma unroll
