@@ -88,7 +88,7 @@ typedef struct icp_engine_hooks {
 
 void icp_params_default(icp_params* p);
 
-/* Full registration on one GPU (device ordinal; -1 = ICP_HIP_DEVICE env or 0).
+/* Full registration on one GPU (device ordinal; -1 = the calling thread's current HIP device).
  * src is rewritten in place on success (engine rules) or always (CLI rules), as the reference. */
 int icp_engine_register(const icp_params* p, double* src_xyz, int64_t n_src, const double* tgt_xyz,
                         int64_t n_tgt, int device, icp_result* res, icp_iteration_record* history,

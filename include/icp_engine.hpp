@@ -47,7 +47,7 @@ struct ICPParameters {
   double sigmaMultiplier = 3.0;
   int octreeMaxPoints = 10;
   int octreeMaxDepth = 20;
-  int device = -1;  // build-only knob: HIP ordinal (-1: $ICP_HIP_DEVICE or 0)
+  int device = -1;  // build-only knob: HIP ordinal (-1: the calling thread's current device)
 };
 
 struct IterationResult {

@@ -37,6 +37,7 @@ extern "C" {
 #define ICP_HIP_EDEVICE (-3)
 #define ICP_HIP_ERCCL (-4)
 #define ICP_HIP_ENOTREADY (-5)
+#define ICP_HIP_EEXCHANGE (-6) /* the host-exchange callback (icp_hip_comm_init_host) failed */
 
 #define ICP_HIP_UNIQUE_ID_BYTES 128
 
@@ -44,6 +45,45 @@ extern "C" {
  * distance and the first-iteration threshold). */
 #define ICP_RULES_ENGINE 0 /* core/icpengine.cpp: best = DBL_MAX, iter-0 relaxed threshold */
 #define ICP_RULES_CLI 1    /* icp_registration.cpp: best = 1e20, threshold mean + 3 std  */
+
+/* Search kernels. Both return the reference's correspondences bit for bit. */
+#define ICP_SEARCH_CERTIFIED 0 /* wave-cooperative search + certificate (the product path)     */
+#define ICP_SEARCH_REFERENCE 1 /* one thread per query, the literal reference-order DFS         */
+
+#define ICP_BUILD_AUTO 0 /* octree built on the device (max_depth <= 21), else on the host       */
+#define ICP_BUILD_HOST 1 /* always the host builder (same arrays bit for bit)                   */
+
+/* Explicit configuration of a context (nothing is read from the environment). Every setting
+ * gives the same correspondences; they select how the device finds them. */
+typedef struct icp_hip_config {
+  int32_t search;         /* ICP_SEARCH_*                                        default CERTIFIED */
+  int32_t scan32;         /* 1: fp32 filter scan + fp64 certificate; 0: fp64 scan      default 1 */
+  int32_t cell_starts;    /* 1: wave walks start from per-level cell tables; 0: root    default 1 */
+  int32_t octree_builder; /* ICP_BUILD_*                                             default AUTO */
+  double join_factor;     /* a query joins its wave's search box if its search radius is at most
+                             join_factor x the wave's mean radius                      default 3.0 */
+  int32_t debug_counters; /* 1: the wave search counts its phases (icp_hip_debug_counters) dflt 0 */
+  int32_t reserved[7];    /* zero */
+} icp_hip_config;
+
+/* Slots of icp_hip_debug_counters (summed over the last iterate's search launches). */
+#define ICP_DBG_WAVES 0          /* waves of the wave search                                  */
+#define ICP_DBG_OVERFLOW 1       /* waves whose candidate set overflowed LDS                   */
+#define ICP_DBG_NOT_JOINED 2     /* lanes with a guess that did not join their wave's box      */
+#define ICP_DBG_NOT_COVERED 3    /* joined lanes whose nearest point was beyond their guess    */
+#define ICP_DBG_RESCAN_POINTS 4  /* points scanned by fp64 re-scans                            */
+#define ICP_DBG_WALK_BATCHES 5   /* walk batches (up to 64 nodes each)                          */
+#define ICP_DBG_NO_GUESS 6       /* lanes without a usable guess                               */
+#define ICP_DBG_CANDIDATES 7     /* candidate points collected by the walks                    */
+#define ICP_DBG_BALL_OVERFLOW 14 /* ball-search queries whose candidate set overflowed         */
+#define ICP_DBG_BALL_POINTS 15   /* points scanned by the ball search                          */
+#define ICP_DBG_CLK_GUESS 16     /* wave clocks (s_memtime): guess + box                       */
+#define ICP_DBG_CLK_WALK 17      /*                          walk                              */
+#define ICP_DBG_CLK_SCAN 18      /*                          scan                              */
+#define ICP_DBG_CLK_FINISH 19    /*                          certify + write + queue           */
+#define ICP_DBG_CLK_START 20     /*                          start nodes (cells or descent)    */
+#define ICP_DBG_START_NODES 21   /* start nodes taken from the cell tables / descent levels    */
+#define ICP_DBG_SLOTS 24
 
 typedef struct icp_hip_ctx icp_hip_ctx;
 
@@ -71,12 +111,18 @@ typedef struct icp_iter_stats {
 
 int icp_hip_device_count(int* count);
 
-/* Create a context on `device` (HIP ordinal). */
+void icp_hip_config_default(icp_hip_config* cfg);
+
+/* Create a context on `device` (HIP ordinal; -1 = the calling thread's current device) with the
+ * default configuration, or with `cfg` (null = default). */
 int icp_hip_create(icp_hip_ctx** out, int device);
+int icp_hip_create_ex(icp_hip_ctx** out, int device, const icp_hip_config* cfg);
 void icp_hip_destroy(icp_hip_ctx* ctx);
 
 /* Multi-GPU: rank 0 calls get_unique_id, the caller distributes the bytes (any side channel),
- * then every rank calls comm_init. Without it a context is a world of one. */
+ * then every rank calls comm_init. Without it a context is a world of one. A communicator of
+ * one rank (nranks = 1) is created as well: every iteration then runs the multi-rank path
+ * (RCCL all-gathers + rank-order merges) on a world of one. */
 int icp_hip_get_unique_id(uint8_t out[ICP_HIP_UNIQUE_ID_BYTES]);
 int icp_hip_comm_init(icp_hip_ctx* ctx, int nranks, int rank, const uint8_t id[ICP_HIP_UNIQUE_ID_BYTES]);
 
@@ -85,13 +131,15 @@ int icp_hip_comm_init(icp_hip_ctx* ctx, int nranks, int rank, const uint8_t id[I
  * rank's record in rank order (nranks x count); it returns 0 on success. The rest of the
  * multi-rank path (rank-order merge on the device, publish) is the one comm_init runs. Used to
  * rehearse several ranks on one GPU (RCCL refuses two ranks on one device) and by callers that
- * already own a host transport. Slower than RCCL: the stream is synchronised around each call. */
+ * already own a host transport. Slower than RCCL: the stream is synchronised around each call.
+ * A failing callback makes icp_hip_iterate return ICP_HIP_EEXCHANGE; the peer ranks are then
+ * left waiting inside their own exchange, and the caller must tear them down. */
 typedef int (*icp_hip_exchange_fn)(void* user, const double* local, int32_t count, double* gathered);
 int icp_hip_comm_init_host(icp_hip_ctx* ctx, int nranks, int rank, icp_hip_exchange_fn exchange, void* user);
 
 /* Build the reference octree of the target (AoS xyz, n points) and keep it in HBM. The tree is
- * built on the device (max_depth <= 21; env ICP_OCTREE_BUILD=host forces the host builder) or on
- * the host (deeper trees); both produce the same arrays bit for bit. rules selects the initial
+ * built on the device (max_depth <= 21, config octree_builder AUTO) or on the host (deeper
+ * trees, or ICP_BUILD_HOST); both produce the same arrays bit for bit. rules selects the initial
  * best distance of findNearest. Non-finite target coordinates and empty targets are rejected
  * (ICP_HIP_EINVAL). Replaces Octree::Octree(points, max_pts, max_d), octree.cpp:41-126. */
 int icp_hip_set_target(icp_hip_ctx* ctx, const double* xyz, int64_t n, int max_points, int max_depth,
@@ -143,6 +191,10 @@ int icp_hip_last_timing(icp_hip_ctx* ctx, double* nn_kernel_ms, double* iterate_
 
 /* The same for each of the last k iterates (k <= 64), oldest first. Waits for them to finish. */
 int icp_hip_timings(icp_hip_ctx* ctx, int k, double* nn_kernel_ms, double* iterate_device_ms);
+
+/* The wave search's diagnostic counters of the last iterate (ICP_DBG_* slots); zeros unless the
+ * context was created with debug_counters = 1. */
+int icp_hip_debug_counters(icp_hip_ctx* ctx, uint64_t out[ICP_DBG_SLOTS]);
 
 int icp_hip_synchronize(icp_hip_ctx* ctx);
 

@@ -10,6 +10,8 @@ from ._lib import (  # noqa: F401
     LIB_PATH,
     IcpError,
     Context,
+    HipConfig,
+    config,
     lib,
     build,
     params_default,
@@ -35,4 +37,9 @@ from ._lib import (  # noqa: F401
     RULES_ENGINE,
     RULES_CLI,
     FLAG_NO_EARLY_STOP,
+    SEARCH_CERTIFIED,
+    SEARCH_REFERENCE,
+    BUILD_AUTO,
+    BUILD_HOST,
+    DBG_NAMES,
 )

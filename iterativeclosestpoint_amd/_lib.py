@@ -15,6 +15,16 @@ LIB_PATH = Path(os.environ.get("ICP_HIP_LIB", PKG_DIR / "libicp_hip.so"))  # ove
 RULES_ENGINE = 0
 RULES_CLI = 1
 FLAG_NO_EARLY_STOP = 1
+SEARCH_CERTIFIED = 0
+SEARCH_REFERENCE = 1
+BUILD_AUTO = 0
+BUILD_HOST = 1
+DBG_SLOTS = 24
+# icp_hip.h ICP_DBG_* slot names
+DBG_NAMES = {0: "waves", 1: "overflow_waves", 2: "not_joined", 3: "not_covered", 4: "rescan_points",
+             5: "walk_batches", 6: "no_guess", 7: "candidates", 14: "ball_overflow", 15: "ball_points",
+             16: "clk_guess", 17: "clk_walk", 18: "clk_scan", 19: "clk_finish", 20: "clk_start",
+             21: "start_nodes"}
 
 _P = C.c_void_p
 _D = C.POINTER(C.c_double)
@@ -42,6 +52,15 @@ class IterStats(C.Structure):
             v = getattr(self, name)
             out[name] = list(v) if not isinstance(v, (int, float)) else v
         return out
+
+
+class HipConfig(C.Structure):
+    """icp_hip_config (include/icp_hip.h): explicit search options of a context."""
+    _fields_ = [
+        ("search", C.c_int32), ("scan32", C.c_int32), ("cell_starts", C.c_int32),
+        ("octree_builder", C.c_int32), ("join_factor", C.c_double), ("debug_counters", C.c_int32),
+        ("reserved", C.c_int32 * 7),
+    ]
 
 
 class Params(C.Structure):
@@ -110,7 +129,10 @@ _EXCHANGE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_double), C.c_int32
 SIGNATURES = {
     # icp_hip.h
     "icp_hip_device_count": (C.c_int, [C.POINTER(C.c_int)]),
+    "icp_hip_config_default": (None, [C.POINTER(HipConfig)]),
     "icp_hip_create": (C.c_int, [C.POINTER(C.c_void_p), C.c_int]),
+    "icp_hip_create_ex": (C.c_int, [C.POINTER(C.c_void_p), C.c_int, C.POINTER(HipConfig)]),
+    "icp_hip_debug_counters": (C.c_int, [_P, _P]),
     "icp_hip_destroy": (None, [_P]),
     "icp_hip_get_unique_id": (C.c_int, [C.c_char_p]),
     "icp_hip_comm_init": (C.c_int, [_P, C.c_int, C.c_int, C.c_char_p]),
@@ -227,12 +249,29 @@ def params_default(**kw) -> Params:
     return p
 
 
-class Context:
-    """One GPU context (icp_hip_ctx) — see include/icp_hip.h."""
+def config(**kw) -> HipConfig:
+    """icp_hip_config with the library defaults, then the given fields."""
+    c = HipConfig()
+    lib().icp_hip_config_default(C.byref(c))
+    for k, v in kw.items():
+        if not hasattr(c, k):
+            raise KeyError(f"icp_hip_config has no field {k!r}")
+        setattr(c, k, v)
+    return c
 
-    def __init__(self, device: int = 0):
+
+class Context:
+    """One GPU context (icp_hip_ctx) — see include/icp_hip.h. `cfg` is an icp_hip_config (or a
+    dict of its fields); None = the library defaults."""
+
+    def __init__(self, device: int = 0, cfg=None):
         self._h = C.c_void_p()
-        _check(lib().icp_hip_create(C.byref(self._h), device))
+        if isinstance(cfg, dict):
+            cfg = config(**cfg)
+        if cfg is None:
+            _check(lib().icp_hip_create(C.byref(self._h), device))
+        else:
+            _check(lib().icp_hip_create_ex(C.byref(self._h), device, C.byref(cfg)))
         self.n_src = 0
 
     def close(self):
@@ -365,6 +404,12 @@ class Context:
 
     def synchronize(self):
         _check(lib().icp_hip_synchronize(self._h))
+
+    def debug_counters(self) -> dict:
+        """The wave search's diagnostic counters of the last iterate (needs debug_counters=1)."""
+        out = np.zeros(DBG_SLOTS, np.uint64)
+        _check(lib().icp_hip_debug_counters(self._h, _ptr(out)))
+        return {name: int(out[k]) for k, name in DBG_NAMES.items()}
 
     def session(self, params: Params) -> "Session":
         return Session(self, params)

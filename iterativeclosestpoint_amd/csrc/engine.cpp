@@ -39,12 +39,6 @@ void log_msg(const icp_engine_hooks* h, const char* fmt, ...) {
   h->on_log(h->user, buf);
 }
 
-int resolve_device(int device) {
-  if (device >= 0) return device;
-  const char* env = std::getenv("ICP_HIP_DEVICE");
-  return env ? std::atoi(env) : 0;
-}
-
 }  // namespace
 
 extern "C" {
@@ -325,7 +319,7 @@ int icp_engine_register(const icp_params* p, double* src, int64_t n_src, const d
   }
   const bool cli = p->rules == ICP_RULES_CLI;
   icp_hip_ctx* ctx = nullptr;
-  int rc = icp_hip_create(&ctx, resolve_device(device));
+  int rc = icp_hip_create(&ctx, device);
   if (rc == ICP_HIP_OK)
     rc = icp_hip_set_target(ctx, tgt, n_tgt, cli ? 10 : p->octree_max_points, cli ? 20 : p->octree_max_depth,
                             p->rules);

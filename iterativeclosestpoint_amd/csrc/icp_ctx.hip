@@ -14,6 +14,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstdio>
+#include <atomic>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -89,6 +90,31 @@ static void free_target(icp_hip_ctx* c) {
   c->n_tgt = 0;
 }
 
+// The search launch over the resident target with this context's configuration; the caller
+// fills the query arrays and the lists.
+static NNLaunch base_launch(const icp_hip_ctx* c) {
+  NNLaunch a;
+  std::memset(&a, 0, sizeof(a));
+  a.nodes = c->nodes;
+  a.pts = c->pts;
+  a.counters = c->counters;
+  a.n_nodes = (int32_t)c->n_nodes;
+  a.pos0 = c->pos0;
+  a.levels = c->levels;
+  a.init_best = c->init_best;
+  a.search = c->cfg.search;
+  a.scan32 = c->cfg.scan32;
+  a.cells = c->cells;
+  a.cell_lmax = c->cell_lmax;
+  a.join_factor = c->cfg.join_factor;
+  a.dbg = c->dbg;
+  for (int k = 0; k < 3; k++) {
+    a.root_lo[k] = c->root_box[k];
+    a.root_hi[k] = c->root_box[3 + k];
+  }
+  return a;
+}
+
 extern "C" {
 
 int icp_hip_device_count(int* count) {
@@ -96,26 +122,41 @@ int icp_hip_device_count(int* count) {
   return ICP_HIP_OK;
 }
 
-int icp_hip_create(icp_hip_ctx** out, int device) {
+void icp_hip_config_default(icp_hip_config* cfg) {
+  if (!cfg) return;
+  std::memset(cfg, 0, sizeof(*cfg));
+  cfg->search = ICP_SEARCH_CERTIFIED;
+  cfg->scan32 = 1;
+  cfg->cell_starts = 1;
+  cfg->octree_builder = ICP_BUILD_AUTO;
+  cfg->join_factor = 3.0;
+  cfg->debug_counters = 0;
+}
+
+int icp_hip_create(icp_hip_ctx** out, int device) { return icp_hip_create_ex(out, device, nullptr); }
+
+int icp_hip_create_ex(icp_hip_ctx** out, int device, const icp_hip_config* cfg) {
   if (!out) return fail(ICP_HIP_EINVAL, "null out");
   *out = nullptr;
+  icp_hip_config conf;
+  icp_hip_config_default(&conf);
+  if (cfg) conf = *cfg;
+  if (conf.search != ICP_SEARCH_CERTIFIED && conf.search != ICP_SEARCH_REFERENCE)
+    return fail(ICP_HIP_EINVAL, "config: unknown search");
+  if (conf.octree_builder != ICP_BUILD_AUTO && conf.octree_builder != ICP_BUILD_HOST)
+    return fail(ICP_HIP_EINVAL, "config: unknown octree builder");
+  if (!(conf.join_factor >= 1.0 && conf.join_factor <= 1e6))
+    return fail(ICP_HIP_EINVAL, "config: join_factor out of [1, 1e6]");
   int ndev = 0;
   hipError_t e = hipGetDeviceCount(&ndev);
   if (e != hipSuccess || ndev == 0)
     return fail(ICP_HIP_EDEVICE, std::string("no HIP device available: ") + hipGetErrorString(e));
-  if (device < 0 || device >= ndev) return fail(ICP_HIP_EINVAL, "device ordinal out of range");
+  if (device < 0) HIP_TRY(hipGetDevice(&device));
+  if (device >= ndev) return fail(ICP_HIP_EINVAL, "device ordinal out of range");
   HIP_TRY(hipSetDevice(device));
   icp_hip_ctx* c = new icp_hip_ctx();
   c->device = device;
-  if (const char* v = std::getenv("ICP_NN_VARIANT")) c->nn_variant = std::atoi(v);
-  if (const char* v = std::getenv("ICP_SCAN_GROUP")) c->scan_group = std::atoi(v);
-  if (const char* v = std::getenv("ICP_WAVE_POINTS")) c->wave_points = std::atoi(v);
-  if (const char* v = std::getenv("ICP_SCAN32")) c->scan32 = std::atoi(v);
-  if (const char* v = std::getenv("ICP_LCA")) c->lca_descent = std::atoi(v);
-  if (const char* v = std::getenv("ICP_CELLS")) c->use_cells = std::atoi(v);
-  if (const char* v = std::getenv("ICP_XCD")) c->xcd_remap = std::atoi(v);
-  if (const char* v = std::getenv("ICP_BALL_GROUPS")) c->ball_groups = std::atoi(v);
-  if (const char* v = std::getenv("ICP_JOIN")) c->join_factor = std::atof(v);
+  c->cfg = conf;
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
     delete c;
     return fail(ICP_HIP_EDEVICE, "hipStreamCreate failed");
@@ -127,13 +168,14 @@ int icp_hip_create(icp_hip_ctx** out, int device) {
       hipHostMalloc(reinterpret_cast<void**>(&c->h_it), sizeof(IterDev), hipHostMallocMapped | hipHostMallocCoherent) !=
           hipSuccess ||
       hipHostGetDevicePointer(reinterpret_cast<void**>(&c->h_it_dev), c->h_it, 0) != hipSuccess ||
-      dalloc(&c->counters, 2) != hipSuccess || dalloc(&c->Tbuf, 16) != hipSuccess ||
-      dalloc(&c->fb_count, 3) != hipSuccess) {
+      dalloc(&c->counters, 2) != hipSuccess || dalloc(&c->fb_count, 3) != hipSuccess ||
+      (conf.debug_counters && dalloc(&c->dbg, ICP_DBG_SLOTS) != hipSuccess)) {
     icp_hip_destroy(c);
     return fail(ICP_HIP_ENOMEM, "context allocation failed");
   }
   (void)hipMemset(c->it, 0, sizeof(IterDev));
   (void)hipMemset(c->fb_count, 0, 3 * sizeof(unsigned int));
+  if (c->dbg) (void)hipMemset(c->dbg, 0, ICP_DBG_SLOTS * sizeof(unsigned long long));
   std::memset(c->h_it, 0, sizeof(IterDev));
   c->lists_zero = true;
   *out = c;
@@ -148,7 +190,6 @@ void icp_hip_destroy(icp_hip_ctx* c) {
   free_target(c);
   dfree(c->it);
   dfree(c->counters);
-  dfree(c->Tbuf);
   dfree(c->fb_count);
   dfree(c->dbg);
   dfree(c->gm);
@@ -173,22 +214,26 @@ int icp_hip_get_unique_id(uint8_t out[ICP_HIP_UNIQUE_ID_BYTES]) {
 }
 
 int icp_hip_comm_init(icp_hip_ctx* c, int nranks, int rank, const uint8_t id_bytes[ICP_HIP_UNIQUE_ID_BYTES]) {
-  if (!c || nranks < 1 || rank < 0 || rank >= nranks) return fail(ICP_HIP_EINVAL, "bad comm arguments");
+  if (!c || !id_bytes || nranks < 1 || rank < 0 || rank >= nranks) return fail(ICP_HIP_EINVAL, "bad comm arguments");
   HIP_TRY(hipSetDevice(c->device));
-  if (c->comm) {
-    (void)ncclCommDestroy(c->comm);
-    c->comm = nullptr;
-  }
-  c->nranks = nranks;
-  c->rank = rank;
-  if (nranks == 1) return ICP_HIP_OK;
-  ncclUniqueId id;
-  std::memcpy(&id, id_bytes, sizeof(id));
-  RCCL_TRY(ncclCommInitRank(&c->comm, nranks, id, rank));
+  // back to a world of one first: a failure below leaves no stale transport behind
+  if (c->comm) (void)ncclCommDestroy(c->comm);
+  c->comm = nullptr;
+  c->xfn = nullptr;
+  c->xuser = nullptr;
+  c->nranks = 1;
+  c->rank = 0;
   dfree(c->gm);
   dfree(c->gc);
   HIP_TRY(dalloc(&c->gm, (size_t)nranks));
   HIP_TRY(dalloc(&c->gc, (size_t)nranks));
+  ncclUniqueId id;
+  std::memcpy(&id, id_bytes, sizeof(id));
+  ncclComm_t comm = nullptr;
+  RCCL_TRY(ncclCommInitRank(&comm, nranks, id, rank));
+  c->comm = comm;
+  c->nranks = nranks;
+  c->rank = rank;
   return ICP_HIP_OK;
 }
 
@@ -196,19 +241,21 @@ int icp_hip_comm_init_host(icp_hip_ctx* c, int nranks, int rank, icp_hip_exchang
   if (!c || nranks < 1 || rank < 0 || rank >= nranks || (nranks > 1 && !exchange))
     return fail(ICP_HIP_EINVAL, "bad comm arguments");
   HIP_TRY(hipSetDevice(c->device));
-  if (c->comm) {
-    (void)ncclCommDestroy(c->comm);
-    c->comm = nullptr;
-  }
-  c->nranks = nranks;
-  c->rank = rank;
-  c->xfn = nranks > 1 ? exchange : nullptr;
-  c->xuser = user;
-  if (nranks == 1) return ICP_HIP_OK;
+  if (c->comm) (void)ncclCommDestroy(c->comm);
+  c->comm = nullptr;
+  c->xfn = nullptr;
+  c->xuser = nullptr;
+  c->nranks = 1;
+  c->rank = 0;
+  if (!exchange) return ICP_HIP_OK;  // a world of one without a transport
   dfree(c->gm);
   dfree(c->gc);
   HIP_TRY(dalloc(&c->gm, (size_t)nranks));
   HIP_TRY(dalloc(&c->gc, (size_t)nranks));
+  c->xfn = exchange;
+  c->xuser = user;
+  c->nranks = nranks;
+  c->rank = rank;
   return ICP_HIP_OK;
 }
 
@@ -222,7 +269,8 @@ static int all_gather_record(icp_hip_ctx* c, const double* d_local, double* d_ga
   std::vector<double> local((size_t)count), all((size_t)count * c->nranks);
   HIP_TRY(hipMemcpyAsync(local.data(), d_local, sizeof(double) * count, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
-  if (c->xfn(c->xuser, local.data(), count, all.data()) != 0) return fail(ICP_HIP_ERCCL, "host exchange callback failed");
+  if (c->xfn(c->xuser, local.data(), count, all.data()) != 0)
+    return fail(ICP_HIP_EEXCHANGE, "host exchange callback failed");
   HIP_TRY(hipMemcpyAsync(d_gathered, all.data(), sizeof(double) * all.size(), hipMemcpyHostToDevice, s));
   HIP_TRY(hipStreamSynchronize(s));
   return ICP_HIP_OK;
@@ -237,8 +285,7 @@ int icp_hip_set_target(icp_hip_ctx* c, const double* xyz, int64_t n, int max_poi
   free_target(c);
   hipEvent_t e0 = c->ev_it0, e1 = c->ev_it1;
   HIP_TRY(hipEventRecord(e0, c->stream));
-  const char* mode = std::getenv("ICP_OCTREE_BUILD");  // "host" forces the host builder (A/B, tests)
-  const bool on_device = max_depth <= kGpuBuildMaxDepth && !(mode && std::strcmp(mode, "host") == 0);
+  const bool on_device = max_depth <= kGpuBuildMaxDepth && c->cfg.octree_builder == ICP_BUILD_AUTO;
   if (on_device) {
     // device build straight from the uploaded AoS cloud (octree_gpu.hip)
     double* d_xyz = nullptr;
@@ -285,7 +332,7 @@ int icp_hip_set_target(icp_hip_ctx* c, const double* xyz, int64_t n, int max_poi
       c->root_box[3 + k] = root.hi[k];
     }
   }
-  if (c->use_cells && c->n_nodes < ((int64_t)1 << 26)) {
+  if (c->cfg.cell_starts && c->n_nodes < ((int64_t)1 << 26)) {
     const int lmax = cell_table_depth(c->n_leaves, c->levels - 1);
     HIP_TRY(dalloc(&c->cells, (size_t)cell_table_entries(lmax)));
     HIP_TRY(build_cell_tables(c->nodes, lmax, c->cells, c->stream));
@@ -391,41 +438,17 @@ int icp_hip_iterate(icp_hip_ctx* c, const double* T_apply, int iter, int rules, 
   if (!c || !out) return fail(ICP_HIP_EINVAL, "null argument");
   if (!c->nodes) return fail(ICP_HIP_ENOTREADY, "target not set");
   if (!c->x && c->n_src > 0) return fail(ICP_HIP_ENOTREADY, "source not set");
-  if (c->nranks > 1 && !c->comm && !c->xfn) return fail(ICP_HIP_ENOTREADY, "communicator not initialised");
   HIP_TRY(hipSetDevice(c->device));
   hipStream_t s = c->stream;
   hipEvent_t* ev = c->ring[c->n_iterates % icp_hip_ctx::kTimingRing];
   HIP_TRY(hipEventRecord(ev[0], s));
-  NNLaunch a;
-  std::memset(&a, 0, sizeof(a));
-  a.nodes = c->nodes;
-  a.pts = c->pts;
+  NNLaunch a = base_launch(c);
   a.x = c->x;
   a.y = c->y;
   a.z = c->z;
   a.pos_out = c->pos;
   a.dist_out = c->dist;
-  a.part = nullptr;  // moments: launch_moments below
-  a.counters = c->counters;
   a.n = c->n_src;
-  a.n_nodes = (int32_t)c->n_nodes;
-  a.pos0 = c->pos0;
-  a.levels = c->levels;
-  a.init_best = c->init_best;
-  a.variant = c->nn_variant;
-  a.scan_group = c->scan_group;
-  a.wave_points = c->wave_points;
-  a.scan32 = c->scan32;
-  a.lca_descent = c->lca_descent;
-  a.cells = c->cells;
-  a.cell_lmax = c->cell_lmax;
-  a.xcd_remap = c->xcd_remap;
-  a.ball_groups = c->ball_groups;
-  a.join_factor = c->join_factor;
-  for (int k = 0; k < 3; k++) {
-    a.root_lo[k] = c->root_box[k];
-    a.root_hi[k] = c->root_box[3 + k];
-  }
   a.apply = T_apply ? 1 : 0;
   if (T_apply)
     for (int k = 0; k < 12; k++) a.T[k] = T_apply[k];
@@ -437,19 +460,14 @@ int icp_hip_iterate(icp_hip_ctx* c, const double* T_apply, int iter, int rules, 
   a.have_prev = c->have_prev ? 1 : 0;
   if (!c->lists_zero) HIP_TRY(hipMemsetAsync(c->fb_count, 0, 3 * sizeof(unsigned int), s));
   c->lists_zero = false;
-  if (std::getenv("ICP_NN_DEBUG")) {
-    if (!c->dbg) HIP_TRY(dalloc(&c->dbg, 24));
-    HIP_TRY(hipMemsetAsync(c->dbg, 0, 24 * sizeof(unsigned long long), s));
-    a.dbg = c->dbg;
-  }
+  if (c->dbg) HIP_TRY(hipMemsetAsync(c->dbg, 0, ICP_DBG_SLOTS * sizeof(unsigned long long), s));
   HIP_TRY(hipEventRecord(ev[1], s));
-  a.ev_fast_done = c->nn_variant >= 3 ? ev[2] : nullptr;
+  a.ev_fast_done = ev[2];
   HIP_TRY(launch_nn(a, s));
-  if (c->nn_variant < 3) HIP_TRY(hipEventRecord(ev[2], s));
-  // residual moments -> mean, std, threshold (one rank: fused into the last merge level)
-  const bool multi = c->nranks > 1;
+  // residual moments -> mean, std, threshold (no communicator: fused into the last merge level)
+  const bool multi = c->comm != nullptr || c->xfn != nullptr;
   const MomentsFinalize fin{sigma_multiplier, iter, rules == ICP_RULES_ENGINE ? 1 : 0};
-  HIP_TRY(launch_moments(c->dist, c->n_src, c->it, c->mparts, s));
+  HIP_TRY(launch_moments(c->dist, c->n_src, c->mparts, s));
   HIP_TRY(launch_merge_moments(c->mparts, c->nb_mom, c->dist, c->n_src, c->it, multi ? nullptr : &fin, s));
   if (multi) {
     const int rc = all_gather_record(c, reinterpret_cast<const double*>(&c->it->m_local),
@@ -467,7 +485,6 @@ int icp_hip_iterate(icp_hip_ctx* c, const double* T_apply, int iter, int rules, 
   cl.it = c->it;
   cl.part = c->cparts;
   cl.n = c->n_src;
-  cl.xcd_remap = c->xcd_remap;
   HIP_TRY(launch_cull_cov(cl, s));
   // covariance moments -> RMSE; the finished record is stored into pinned host memory
   const uint64_t seq = ++c->publish_seq;
@@ -481,17 +498,21 @@ int icp_hip_iterate(icp_hip_ctx* c, const double* T_apply, int iter, int rules, 
   }
   HIP_TRY(hipEventRecord(ev[3], s));
   c->n_iterates++;
-  // The host's only wait of the iteration: the publishing kernel's last store is the sequence
-  // number (after a system-scope fence), so the record is complete once it shows up. Polling
-  // the pinned word wakes the host within ~1 us; the stream is queried between polls so a
-  // device error still surfaces.
+  // The host's only wait of the iteration: the publishing kernel stores the record with
+  // system-scope stores, waits for their acknowledgement, then stores the sequence word (no
+  // fence; reduce_kernels.hip finalize_cov_publish). Polling the pinned word wakes the host within
+  // ~1 us; the stream is queried between polls so a device error still surfaces. The word is read
+  // with acquire ordering, so the record's words are read after it.
   {
-    const volatile double* flag = &c->h_it->pad[3];
     const double want = (double)seq;
-    for (unsigned spin = 1; *flag != want; spin++) {
+    uint64_t want_bits;
+    std::memcpy(&want_bits, &want, sizeof(want));
+    const uint64_t* word = reinterpret_cast<const uint64_t*>(&c->h_it->pad[3]);
+    auto published = [&]() { return __atomic_load_n(word, __ATOMIC_ACQUIRE) == want_bits; };
+    for (unsigned spin = 1; !published(); spin++) {
       if ((spin & 1023u) == 0) {
         const hipError_t q = hipStreamQuery(s);
-        if (q == hipSuccess && *flag == want) break;
+        if (q == hipSuccess && published()) break;
         if (q == hipSuccess) return fail(ICP_HIP_EDEVICE, "iterate: stream idle but the record was not published");
         if (q != hipErrorNotReady) return fail(ICP_HIP_EDEVICE, std::string("iterate: ") + hipGetErrorString(q));
       }
@@ -515,36 +536,22 @@ int icp_hip_iterate(icp_hip_ctx* c, const double* T_apply, int iter, int rules, 
     out->centroid_tgt[k] = h.c_global.mb[k];
   }
   for (int k = 0; k < 9; k++) out->H[k] = h.c_global.c[k];
-  out->n_fallback = c->nn_variant >= 3 ? (int64_t)c->last_lists[0] : 0;
-  out->n_lane_search = c->nn_variant >= 4 ? (int64_t)c->last_lists[2] : 0;
-  out->n_ball_search = c->nn_variant >= 4 ? (int64_t)c->last_lists[1] : 0;
+  const bool cert = c->cfg.search == ICP_SEARCH_CERTIFIED;
+  out->n_fallback = cert ? (int64_t)c->last_lists[0] : 0;
+  out->n_lane_search = cert ? (int64_t)c->last_lists[2] : 0;
+  out->n_ball_search = cert ? (int64_t)c->last_lists[1] : 0;
   c->have_results = true;
   c->have_prev = true;
-  if (c->dbg && std::getenv("ICP_NN_DEBUG")) {
-    unsigned long long h[24];
-    if (hipMemcpy(h, c->dbg, sizeof(h), hipMemcpyDeviceToHost) == hipSuccess) {
-      const double w = h[0] ? (double)h[0] : 1.0;
-      std::fprintf(stderr,
-                   "[icp dbg] iter=%d wave clocks: guess+box=%.0f descent=%.0f walk=%.0f scan=%.0f finish=%.0f "
-                   "descent_levels/wave=%.2f\n",
-                   iter, (double)h[16] / w, (double)h[20] / w, (double)h[17] / w, (double)h[18] / w,
-                   (double)h[19] / w, (double)h[21] / w);
-      const double nl = c->last_lists[2] ? (double)c->last_lists[2] : 1.0;
-      std::fprintf(stderr, "[icp dbg] iter=%d ball_list=%u ball_overflow=%llu ball_pts/query=%.1f lane_list=%u\n", iter,
-                   c->last_lists[1], h[14], c->last_lists[1] ? (double)h[15] / c->last_lists[1] : 0.0,
-                   c->last_lists[2]);
-      std::fprintf(stderr,
-                   "[icp dbg] iter=%d lane_list: visits/query=%.1f max_visits=%llu pts/query=%.1f "
-                   ">256 visits=%llu >1024 visits=%llu max_dist_mm=%llu\n",
-                   iter, (double)h[8] / nl, h[9], (double)h[10] / nl, h[11], h[12], h[13]);
-      std::fprintf(stderr,
-                   "[icp dbg] iter=%d waves=%llu overflow=%llu excluded=%llu coverage_fail=%llu not_cand=%llu "
-                   "cand_pts/wave=%.1f leaves/wave=%.1f bfs_rounds/wave=%.2f lane_list=%u fallback=%u\n",
-                   iter, h[0], h[1], h[2], h[3], h[6], h[0] ? (double)h[4] / h[0] : 0.0,
-                   h[0] ? (double)h[7] / h[0] : 0.0, h[0] ? (double)h[5] / h[0] : 0.0, c->last_lists[1],
-                   c->last_lists[0]);
-    }
-  }
+  return ICP_HIP_OK;
+}
+
+int icp_hip_debug_counters(icp_hip_ctx* c, uint64_t out[ICP_DBG_SLOTS]) {
+  if (!c || !out) return fail(ICP_HIP_EINVAL, "null argument");
+  std::memset(out, 0, ICP_DBG_SLOTS * sizeof(uint64_t));
+  if (!c->dbg) return ICP_HIP_OK;
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipMemcpyAsync(out, c->dbg, ICP_DBG_SLOTS * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
   return ICP_HIP_OK;
 }
 
@@ -605,35 +612,13 @@ int icp_hip_nn(icp_hip_ctx* c, const double* q, int64_t n, int32_t* idx_out, dou
       (e = dalloc(&dd, n)) == hipSuccess && (e = dalloc(&pos, n)) == hipSuccess && (e = dalloc(&di, n)) == hipSuccess) {
     e = hipMemcpyAsync(aos, q, 3 * sizeof(double) * n, hipMemcpyHostToDevice, c->stream);
     if (e == hipSuccess) e = launch_deinterleave(aos, x, y, z, n, c->stream);
-    NNLaunch a;
-    std::memset(&a, 0, sizeof(a));
-    a.nodes = c->nodes;
-    a.pts = c->pts;
+    NNLaunch a = base_launch(c);
     a.x = x;
     a.y = y;
     a.z = z;
     a.pos_out = pos;
     a.dist_out = d;
-    a.part = nullptr;
     a.n = n;
-    a.n_nodes = (int32_t)c->n_nodes;
-    a.pos0 = c->pos0;
-    a.levels = c->levels;
-    a.init_best = c->init_best;
-  a.variant = c->nn_variant;
-  a.scan_group = c->scan_group;
-  a.wave_points = c->wave_points;
-  a.scan32 = c->scan32;
-  a.lca_descent = c->lca_descent;
-  a.cells = c->cells;
-  a.cell_lmax = c->cell_lmax;
-  a.xcd_remap = c->xcd_remap;
-  a.ball_groups = c->ball_groups;
-  a.join_factor = c->join_factor;
-  for (int k = 0; k < 3; k++) {
-    a.root_lo[k] = c->root_box[k];
-    a.root_hi[k] = c->root_box[3 + k];
-  }
     int32_t* fbl = nullptr;
     double* fbu = nullptr;
     if (e == hipSuccess) e = dalloc(&fbl, 3 * (size_t)n);
@@ -666,36 +651,14 @@ int icp_hip_traversal_counts(icp_hip_ctx* c, double* mean_entries, double* mean_
   if (!c->nodes || (!c->x && c->n_src > 0)) return fail(ICP_HIP_ENOTREADY, "target/source not set");
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipMemsetAsync(c->counters, 0, 2 * sizeof(unsigned long long), c->stream));
-  NNLaunch a;
-  std::memset(&a, 0, sizeof(a));
-  a.nodes = c->nodes;
-  a.pts = c->pts;
+  NNLaunch a = base_launch(c);
   a.x = c->x;
   a.y = c->y;
   a.z = c->z;
   a.pos_out = c->pos;  // same queries as the last iterate: identical outputs are rewritten
   a.dist_out = c->dist;
-  a.part = nullptr;
-  a.counters = c->counters;
   a.n = c->n_src;
-  a.n_nodes = (int32_t)c->n_nodes;
-  a.pos0 = c->pos0;
-  a.levels = c->levels;
-  a.init_best = c->init_best;
-  a.variant = c->nn_variant;
-  a.scan_group = c->scan_group;
-  a.wave_points = c->wave_points;
-  a.scan32 = c->scan32;
-  a.lca_descent = c->lca_descent;
-  a.cells = c->cells;
-  a.cell_lmax = c->cell_lmax;
-  a.xcd_remap = c->xcd_remap;
-  a.ball_groups = c->ball_groups;
-  a.join_factor = c->join_factor;
-  for (int k = 0; k < 3; k++) {
-    a.root_lo[k] = c->root_box[k];
-    a.root_hi[k] = c->root_box[3 + k];
-  }
+  a.dbg = nullptr;
   a.count = 1;
   HIP_TRY(launch_nn(a, c->stream));
   unsigned long long h[2] = {0, 0};

@@ -11,15 +11,7 @@
 
 struct icp_hip_ctx {
   int device = 0;
-  int nn_variant = 4;  // search kernel variant (ICP_NN_VARIANT env, for A/B runs)
-  int scan_group = 64; // lanes per scan group of the wave search (ICP_SCAN_GROUP env: 8/16/32/64)
-  int wave_points = 1024; // candidate-list capacity per wave (ICP_WAVE_POINTS env: 512/768/1024)
-  int scan32 = 1;         // fp32 filter scan in the wave search (ICP_SCAN32=0: fp64 scan)
-  int lca_descent = 1;    // uniform descent before the wave's breadth-first walk (ICP_LCA=0: off)
-  int use_cells = 1;      // start the wave walk from the cell tables (ICP_CELLS=0: off)
-  double join_factor = 3.0;  // wave-box join rule: radius <= factor x the wave's mean (ICP_JOIN)
-  int ball_groups = 4;    // queries per wave of the ball search (ICP_BALL_GROUPS=1: one)
-  int xcd_remap = 0;      // XCD-contiguous block order for search and cull (ICP_XCD=1; measured: no gain)
+  icp_hip_config cfg{};  // explicit configuration (icp_hip_create_ex); nothing from the environment
   hipStream_t stream = nullptr;
   hipEvent_t ev_it0 = nullptr, ev_it1 = nullptr;  // set_target timing
   // per-iterate timing events, a ring over the last kTimingRing iterates:
@@ -64,9 +56,8 @@ struct icp_hip_ctx {
   icp::IterDev* h_it_dev = nullptr;  // its device address
   uint64_t publish_seq = 0;          // h_it->pad[3] = seq once the record is complete
   unsigned long long* counters = nullptr;
-  double* Tbuf = nullptr;
 
-  // multi-GPU
+  // multi-GPU (comm or xfn set: every iterate runs the all-gather + rank-order merge path)
   int nranks = 1, rank = 0;
   ncclComm_t comm = nullptr;
   icp_hip_exchange_fn xfn = nullptr;  // host exchange instead of RCCL (icp_hip_comm_init_host)

@@ -1,0 +1,711 @@
+// nn_kernels.hip — gfx950 octree nearest-neighbour search of the ICP correspondence step.
+//
+// Replaces the reference's per-source-point loop over Octree::findNearest
+// (core/icpengine.cpp:169-184 -> octree.cpp:128-184; CLI icp_registration.cpp:481-496).
+// Every kernel returns, for each query, exactly the index and residual the reference DFS returns.
+//
+//  k_nn_ref    one thread per query, the literal reference-order DFS (the parity kernel, and the
+//              work counter of the roofline's "reference work" figure).
+//  k_nn_wave   the product search: 64 spatially coherent queries per wave share one search box,
+//              one cooperative walk of the octree, one lockstep fp32 filter scan, and a rigorous
+//              per-query certificate (nn_device.h) that the reference returns the same point.
+//  k_nn_ball   the queries a wave did not take, four per wave (16-lane groups), sphere walks.
+//  k_nn_lists  the rest: per-lane certified search, else the reference-order DFS.
+//
+// Everything is fp64 except the scan's filter, whose result is re-evaluated in fp64; built with
+// -ffp-contract=off (the reference is built without FMA).
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+
+#include "kernels.h"
+#include "nn_device.h"
+
+namespace icp {
+
+namespace {
+
+using namespace dev;
+
+// ---------------------------------------------------------------------------------------------
+// The reference-order kernel.
+template <bool APPLY, bool COUNT>
+__global__ void __launch_bounds__(256) k_nn_ref(NNLaunch a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned long long lds_stack[];
+  const int bs = blockDim.x;
+  const int64_t i = (int64_t)blockIdx.x * bs + threadIdx.x;
+  const bool active = i < a.n;
+
+  double qx = 0.0, qy = 0.0, qz = 0.0;
+  load_query<APPLY>(a, i, active, qx, qy, qz);
+
+  double best_d2 = a.init_best;
+  int32_t best = -1;
+  double visits = 0.0, scanned = 0.0;
+  // A NaN coordinate makes every leaf distance NaN, so the reference never updates best_idx
+  // (octree.cpp:146): skipping the search is exact. (Its box distances stay finite: max(0,NaN)=0.)
+  const bool nan_q = (qx != qx) || (qy != qy) || (qz != qz);
+  if (active && !nan_q && a.n_nodes > 0)
+    exact_dfs<COUNT>(a, qx, qy, qz, lds_stack + threadIdx.x, bs, best, best_d2, visits, scanned);
+  if (active) {
+    const int32_t pos = best >= 0 ? best : a.pos0;
+    a.pos_out[i] = pos;
+    a.dist_out[i] = best >= 0 ? __builtin_sqrt(best_d2)  // == computeDistance bit for bit
+                              : residual_to(a.pts, a.pos0, qx, qy, qz);
+  }
+  if (COUNT) {
+    __syncthreads();  // every traversal is done: reuse the stack LDS for the reduction
+    double c[2] = {visits, scanned};
+    block_sum<2>(c, reinterpret_cast<double*>(lds_stack));
+    if (threadIdx.x == 0) {
+      atomicAdd(&a.counters[0], (unsigned long long)c[0]);
+      atomicAdd(&a.counters[1], (unsigned long long)c[1]);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// The wave search.
+//
+// The 64 queries of a wave are one kd bucket of the source: spatially compact.
+//  1. Guess u >= each query's nearest squared distance: after an iteration on the same queries,
+//     (previous residual + displacement)^2 (triangle inequality); otherwise one nearest-child
+//     descent to a leaf and its smallest d2.
+//  2. Lanes with radius r = sqrt(u)(1 + 2^-40) + |q| 2^-45 <= join x the wave's mean radius
+//     join one search box B = the bbox of their balls (DPP reductions).
+//  3. The leaves meeting B are collected by a cooperative walk (LIFO stack in LDS, up to 64 nodes
+//     per batch), started from the cell tables (or a wave-uniform descent without them).
+//  4. The points of those leaves that lie in B are staged 64 at a time as fp32 offsets from B's
+//     centre, in pairs, and every joined lane scans them in lockstep (packed fp32), keeping its
+//     two smallest values and the position of the smallest.
+//  5. The winner's fp64 distance is recomputed with the reference arithmetic; every other point's
+//     fl(d2) is bounded below from the second-smallest fp32 value (scan32_lower_bound). A wave
+//     with a lane this cannot certify re-scans in fp64.
+// Each joined lane's ball lies in B, so every point within best (1 + 2^-48) of it was scanned:
+// the certificate of nn_device.h applies. Non-joined lanes go to the ball list, uncertified ones
+// to the exact list.
+constexpr int kWaveQueue = 256;  // node ids of the walk's LIFO stack (staging area after the walk)
+constexpr int kWavePoints = 1024;  // candidate points per wave
+constexpr int kWaveLds = kWaveQueue * 4 + kWavePoints * 4;  // 5 KB per wave
+static_assert(kWaveQueue * 4 >= 64 * 16 && kWaveQueue * 4 >= 32 * 32, "staging area aliases the stack");
+
+// Lower bound of fl64(d2) of every point whose fp32 squared distance (the scan) is >= s32.
+// Coordinates are offsets from B's centre, |offset| <= ext for points and joined queries. With
+// u = 2^-24: each fp32 offset differs from the exact one by <= ext (u + 2^-53) =: ext k; the fp32
+// difference dx' = (p' - q')(1 + e), |e| <= u, so |dx' - dx| <= 2 ext k + u |dx| + ..., and over
+// three axes |‖d'‖ - D| <= e_abs + u D with e_abs = sqrt(3) 2 ext k (1 + u). The fp32 sum of
+// squares (one mul, two fma) is ‖d'‖^2 (1 + t), |t| <= (1 + u)^3 - 1, plus <= 3 2^-126 of
+// underflow. Hence D >= (sqrt((s32 - 2^-120) / (1 + 3.0001 u)) - e_abs) / (1 + u), and
+// fl64(d2) >= D^2 (1 - 5 2^-53). Every step rounds towards the bound by an explicit 2^-50 margin.
+__device__ __forceinline__ double scan32_lower_bound(float s32, double ext) {
+  if (!(s32 < __builtin_inff())) return __builtin_inf();
+  const double u = 0x1p-24;
+  const double e_abs = 1.7320509 * 2.0 * ext * (u * (1.0 + 0x1p-20)) * (1.0 + u) * (1.0 + 0x1p-40);
+  double n2 = ((double)s32 - 0x1p-120) / (1.0 + 3.0001 * u);
+  if (!(n2 > 0.0)) return 0.0;
+  const double n = __builtin_sqrt(n2) * (1.0 - 0x1p-50);
+  double d = (n - e_abs) / (1.0 + u) * (1.0 - 0x1p-50);
+  if (!(d > 0.0)) return 0.0;
+  return d * d * (1.0 - 0x1p-48);
+}
+
+template <bool APPLY>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) k_nn_wave(NNLaunch a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned long long lds_raw[];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool active = i < a.n;
+  unsigned char* wl = reinterpret_cast<unsigned char*>(lds_raw) + wv * kWaveLds;
+  int32_t* queue = reinterpret_cast<int32_t*>(wl);
+  double4* stage = reinterpret_cast<double4*>(wl);  // after the walk only
+  int32_t* plist = queue + kWaveQueue;               // candidate points
+
+  double qx = 0.0, qy = 0.0, qz = 0.0, ox = 0.0, oy = 0.0, oz = 0.0;
+  if (active) {
+    ox = a.x[i];
+    oy = a.y[i];
+    oz = a.z[i];
+  }
+  load_query<APPLY>(a, i, active, qx, qy, qz);
+  const bool finite_q = __builtin_isfinite(qx) && __builtin_isfinite(qy) && __builtin_isfinite(qz);
+
+  const unsigned long long t_p0 = a.dbg ? __builtin_amdgcn_s_memtime() : 0ull;
+  // Phase 1: the guess (any value is safe: certification also requires best <= u).
+  double u = __builtin_inf();
+  if (active && finite_q && a.have_prev) {
+    const double dp = a.dist_out[i];
+    const double ex = qx - ox, ey = qy - oy, ez = qz - oz;
+    const double g = dp + __builtin_sqrt(ex * ex + ey * ey + ez * ez);
+    u = (g * g) * (1.0 + 0x1p-30);
+  } else if (active && finite_q) {
+    const NodeRec* r0 = a.nodes;
+    double lx = r0->lo[0], ly = r0->lo[1], lz = r0->lo[2], hx = r0->hi[0], hy = r0->hi[1], hz = r0->hi[2];
+    int32_t node = 0;
+    while (true) {
+      const int2 topo = *reinterpret_cast<const int2*>(&a.nodes[node].first);
+      const uint32_t meta = (uint32_t)topo.y;
+      if (meta & kLeafBit) {
+        const int32_t cnt = (int32_t)(meta & ~kLeafBit);
+        for (int32_t k = 0; k < cnt; k++) {
+          const TgtPt* p = a.pts + topo.x + k;
+          const double dx = p->x - qx, dy = p->y - qy, dz = p->z - qz;
+          const double d2 = dx * dx + dy * dy + dz * dz;
+          u = d2 < u ? d2 : u;
+        }
+        break;
+      }
+      const double mx = (lx + hx) / 2, my = (ly + hy) / 2, mz = (lz + hz) / 2;
+      const double ax0 = smax(0.0, smax(lx - qx, qx - mx)), ax1 = smax(0.0, smax(mx - qx, qx - hx));
+      const double ay0 = smax(0.0, smax(ly - qy, qy - my)), ay1 = smax(0.0, smax(my - qy, qy - hy));
+      const double az0 = smax(0.0, smax(lz - qz, qz - mz)), az1 = smax(0.0, smax(mz - qz, qz - hz));
+      const double sx[2] = {ax0 * ax0, ax1 * ax1};
+      const double sy[2] = {ay0 * ay0, ay1 * ay1};
+      const double sz[2] = {az0 * az0, az1 * az1};
+      const uint32_t mask = meta & 0xffu;
+      double bs_ = __builtin_inf();
+      uint32_t o1 = 0;
+#pragma unroll
+      for (int o = 0; o < 8; o++) {
+        const double c = sx[o & 1] + sy[(o >> 1) & 1] + sz[o >> 2];
+        const bool take = ((mask >> o) & 1u) && c < bs_;
+        bs_ = take ? c : bs_;
+        o1 = take ? (uint32_t)o : o1;
+      }
+      node = topo.x + __builtin_popcount(mask & ((1u << o1) - 1u));
+      if (o1 & 1u) lx = mx; else hx = mx;
+      if (o1 & 2u) ly = my; else hy = my;
+      if (o1 & 4u) lz = mz; else hz = mz;
+    }
+  }
+
+  // Phase 2: the wave's search box over the lanes that join.
+  const bool cand = active && finite_q && u <= 0x1p900;
+  const double amax = __builtin_fmax(__builtin_fabs(qx), __builtin_fmax(__builtin_fabs(qy), __builtin_fabs(qz)));
+  const double r = cand ? __builtin_sqrt(u) * (1.0 + 0x1p-40) + amax * 0x1p-45 : 0.0;
+  const unsigned long long cmask = __ballot(cand);
+  const double mean_r = wave_sum_d(r) / (double)(cmask ? __popcll(cmask) : 1);
+  bool join = cand && r <= a.join_factor * mean_r;
+  const double blx = wave_min_d(join ? qx - r : __builtin_inf());
+  const double bly = wave_min_d(join ? qy - r : __builtin_inf());
+  const double blz = wave_min_d(join ? qz - r : __builtin_inf());
+  const double bhx = wave_max_d(join ? qx + r : -__builtin_inf());
+  const double bhy = wave_max_d(join ? qy + r : -__builtin_inf());
+  const double bhz = wave_max_d(join ? qz + r : -__builtin_inf());
+
+  const unsigned long long t_p2 = a.dbg ? __builtin_amdgcn_s_memtime() : 0ull;
+  unsigned long long t_pd = t_p2;
+  // Phase 3: the leaves meeting B.
+  int nleaf = 0;
+  bool overflow = false;
+  if (__ballot(join) != 0) {
+    int tail = 1;
+    if (a.cells) {
+      tail = cell_starts<64>(a, blx, bly, blz, bhx, bhy, bhz, lane, 0, queue);
+      if (a.dbg && lane == 0) atomicAdd(&a.dbg[21], (unsigned long long)tail);
+    } else {
+      // Wave-uniform descent to the deepest node that holds every leaf meeting B: follow the
+      // only child meeting B while there is exactly one.
+      int32_t start = 0;
+      while (true) {
+        const NodeRec* rr = a.nodes + start;
+        const int2 topo = *reinterpret_cast<const int2*>(&rr->first);
+        const uint32_t meta = (uint32_t)topo.y;
+        if (meta & kLeafBit) break;
+        uint32_t kids = children_in_box(rr, meta & 0xffu, blx, bly, blz, bhx, bhy, bhz);
+        kids = (uint32_t)__builtin_amdgcn_readfirstlane((int)kids);
+        if (__builtin_popcount(kids) != 1) break;
+        const uint32_t o = (uint32_t)__builtin_ctz(kids);
+        start = __builtin_amdgcn_readfirstlane(topo.x + __builtin_popcount((meta & 0xffu) & ((1u << o) - 1u)));
+        if (a.dbg && lane == 0) atomicAdd(&a.dbg[21], 1ull);
+      }
+      if (lane == 0) queue[0] = start;
+    }
+    if (a.dbg) t_pd = __builtin_amdgcn_s_memtime();
+    // Every batch pops up to 64 nodes, which already meet B (tested by their parent; the start
+    // nodes by the cell box or the descent), appends the points of its leaves to the candidate
+    // list and pushes its children meeting B. Most recent first: the live set stays small.
+    wave_lds_fence();
+    while (tail > 0) {
+      const int batch = tail < 64 ? tail : 64;
+      const bool has = lane < batch;
+      bool leaf = false;
+      int32_t first = 0;
+      uint32_t meta = 0, kids = 0;
+      if (has) {
+        const NodeRec* rr = a.nodes + queue[tail - batch + lane];
+        const int2 topo = *reinterpret_cast<const int2*>(&rr->first);
+        first = topo.x;
+        meta = (uint32_t)topo.y;
+        leaf = (meta & kLeafBit) != 0;
+        if (!leaf) kids = children_in_box(rr, meta & 0xffu, blx, bly, blz, bhx, bhy, bhz);
+      }
+      // a leaf contributes its points (contiguous in leaf order) to the candidate list
+      const int lcnt = (has && leaf) ? (int)(meta & ~kLeafBit) : 0;
+      int ltot;
+      const int lincl = wave_incl_scan(lcnt, &ltot);
+      const int lpos = nleaf + lincl - lcnt;
+      if (lcnt > 0 && lpos + lcnt <= kWavePoints)
+        for (int c = 0; c < lcnt; c++) plist[lpos + c] = first + c;
+      nleaf += ltot;
+      const int nch = __builtin_popcount(kids);
+      int tot;
+      const int incl = wave_incl_scan(nch, &tot);
+      tail -= batch;  // the popped entries are in registers; children overwrite them
+      if (nleaf > kWavePoints || tail + tot > kWaveQueue) {
+        overflow = true;
+        break;
+      }
+      int off = tail + incl - nch;
+      const uint32_t mask = meta & 0xffu;
+      uint32_t kk = kids;
+      while (kk) {
+        const uint32_t o = (uint32_t)__builtin_ctz(kk);
+        kk &= kk - 1u;
+        queue[off++] = first + __builtin_popcount(mask & ((1u << o) - 1u));
+      }
+      tail += tot;
+      if (a.dbg && lane == 0) atomicAdd(&a.dbg[5], 1ull);
+      wave_lds_fence();
+    }
+  }
+  if (overflow) join = false;
+  if (a.dbg && lane == 0) {
+    atomicAdd(&a.dbg[0], 1ull);
+    if (overflow) atomicAdd(&a.dbg[1], 1ull);
+  }
+
+  const unsigned long long t_p3 = a.dbg ? __builtin_amdgcn_s_memtime() : 0ull;
+  // Phase 4: the lockstep scan: 64 candidates per chunk are gathered by one load per lane (the
+  // next chunk's gather is in flight while the current one is scanned from LDS).
+  double best = __builtin_inf(), second = __builtin_inf();
+  int32_t bpos = -1;
+  const int npts = nleaf;
+  int scanned_pts = 0;
+  bool need64 = __ballot(join) != 0 && npts > 0;
+  if (a.scan32 && need64) {
+    const double ocx = (blx + bhx) * 0.5, ocy = (bly + bhy) * 0.5, ocz = (blz + bhz) * 0.5;
+    const double ext = dmax_(dmax_(dmax_(bhx - ocx, ocx - blx), dmax_(bhy - ocy, ocy - bly)),
+                             dmax_(bhz - ocz, ocz - blz)) * (1.0 + 0x1p-40);
+    if (ext >= 0x1p-40 && ext <= 0x1p60) {
+      const float qx32 = (float)(qx - ocx), qy32 = (float)(qy - ocy), qz32 = (float)(qz - ocz);
+      // staging area: points in pairs, [x0 x1 y0 y1 z0 z1 w0 w1] (32 B), so that one packed fp32
+      // instruction (v_pk_add/mul/fma_f32) evaluates an axis of two points
+      float* stage32 = reinterpret_cast<float*>(wl);
+      float s1 = __builtin_inff(), s2 = __builtin_inff();
+      int32_t p1 = -1;
+      wave_lds_fence();
+      double4 nxtp = make_double4(0.0, 0.0, 0.0, 0.0);
+      if (lane < npts) {
+        const int32_t g = plist[lane];
+        const TgtPt* p = a.pts + g;
+        const double2 xy = *reinterpret_cast<const double2*>(&p->x);
+        nxtp = make_double4(xy.x, xy.y, p->z, __longlong_as_double((long long)g));
+      }
+      for (int base = 0; base < npts; base += 64) {
+        const bool nin = base + lane < npts && nxtp.x >= blx && nxtp.x <= bhx && nxtp.y >= bly && nxtp.y <= bhy &&
+                         nxtp.z >= blz && nxtp.z <= bhz;
+        const unsigned long long im = __ballot(nin);
+        const int slot = mask_rank(im);
+        const float vx = (float)(nxtp.x - ocx), vy = (float)(nxtp.y - ocy), vz = (float)(nxtp.z - ocz);
+        const float vw = __int_as_float((int)__double_as_longlong(nxtp.w));
+        const int m = __popcll(im);
+        wave_lds_fence();  // previous chunk's reads are done before overwriting the staging slots
+        if (nin) {
+          float* sp = stage32 + 8 * (slot >> 1) + (slot & 1);
+          sp[0] = vx;
+          sp[2] = vy;
+          sp[4] = vz;
+          sp[6] = vw;
+        }
+        if ((m & 1) && lane == 63) {
+          // odd count: the last pair's second point at +inf (its sq = +inf never replaces s1 and
+          // leaves s2 unchanged; no NaN can arise from inf - finite)
+          float* sp = stage32 + 8 * (m >> 1) + 1;
+          sp[0] = __builtin_inff();
+          sp[2] = __builtin_inff();
+          sp[4] = __builtin_inff();
+        }
+        wave_lds_fence();
+        const int nb = base + 64;
+        if (nb + lane < npts) {
+          const int32_t g = plist[nb + lane];
+          const TgtPt* p = a.pts + g;
+          const double2 xy = *reinterpret_cast<const double2*>(&p->x);
+          nxtp = make_double4(xy.x, xy.y, p->z, __longlong_as_double((long long)g));
+        }
+        scanned_pts += m;
+        // lockstep over the staged pairs (16-B broadcast reads). Point 2k is selected before point
+        // 2k + 1: the same sequence of updates as a one-point-at-a-time scan.
+        typedef float f2 __attribute__((ext_vector_type(2)));
+        typedef int v4i __attribute__((ext_vector_type(4)));
+        const f2 qx2 = {qx32, qx32}, qy2 = {qy32, qy32}, qz2 = {qz32, qz32};
+        auto sel = [&](float sq, int w) {
+          const bool lt = sq < s1;
+          s2 = __builtin_amdgcn_fmed3f(s1, s2, sq);
+          s1 = lt ? sq : s1;
+          p1 = lt ? w : p1;
+        };
+        auto eval2 = [&](const v4i xy, const v4i zw) {
+          const f2 X = {__int_as_float(xy.x), __int_as_float(xy.y)};
+          const f2 Y = {__int_as_float(xy.z), __int_as_float(xy.w)};
+          const f2 Z = {__int_as_float(zw.x), __int_as_float(zw.y)};
+          const f2 dx = X - qx2, dy = Y - qy2, dz = Z - qz2;
+          const f2 sq = __builtin_elementwise_fma(dz, dz, __builtin_elementwise_fma(dy, dy, dx * dx));
+          sel(sq.x, zw.z);
+          sel(sq.y, zw.w);
+        };
+        const v4i* st4 = reinterpret_cast<const v4i*>(stage32);
+        const int mp = (m + 1) >> 1;
+        int k = 0;
+        for (; k + 2 <= mp; k += 2) {
+          const v4i a0 = st4[2 * k], b0 = st4[2 * k + 1], a1 = st4[2 * k + 2], b1 = st4[2 * k + 3];
+          eval2(a0, b0);
+          eval2(a1, b1);
+        }
+        if (k < mp) eval2(st4[2 * k], st4[2 * k + 1]);
+      }
+      // fp64 distance of the fp32 winner, exactly as the leaf scan computes it (octree.cpp:139-144)
+      double b64 = __builtin_inf();
+      if (join && p1 >= 0) {
+        const TgtPt* p = a.pts + p1;
+        const double dx = p->x - qx, dy = p->y - qy, dz = p->z - qz;
+        b64 = dx * dx + dy * dy + dz * dz;
+      }
+      const double lb2 = scan32_lower_bound(s2, ext);
+      // a lane whose fp32 winner is not within its guess goes to the per-lane search either way
+      const bool ok = !join || p1 < 0 || !(b64 <= u) || certified(b64, lb2, a.init_best);
+      if (__ballot(!ok) == 0) {
+        best = b64;
+        second = lb2;
+        bpos = p1;
+        need64 = false;
+      }
+    }
+  }
+  if (need64) {
+    // Points outside B are farther than r from every joined lane (each ball lies in B), so
+    // they can neither be a joined lane's nearest point nor sit in its certificate window.
+    wave_lds_fence();
+    double4 nxtp = make_double4(0.0, 0.0, 0.0, 0.0);
+    bool nin = false;
+    if (lane < npts) {
+      const int32_t g = plist[lane];
+      const TgtPt* p = a.pts + g;
+      const double2 xy = *reinterpret_cast<const double2*>(&p->x);
+      nxtp = make_double4(xy.x, xy.y, p->z, __longlong_as_double((long long)g));
+    }
+    for (int base = 0; base < npts; base += 64) {
+      nin = base + lane < npts && nxtp.x >= blx && nxtp.x <= bhx && nxtp.y >= bly && nxtp.y <= bhy &&
+            nxtp.z >= blz && nxtp.z <= bhz;
+      const unsigned long long im = __ballot(nin);
+      const int slot = mask_rank(im);
+      const double4 cur = nxtp;
+      const int nb = base + 64;
+      if (nb + lane < npts) {
+        const int32_t g = plist[nb + lane];
+        const TgtPt* p = a.pts + g;
+        const double2 xy = *reinterpret_cast<const double2*>(&p->x);
+        nxtp = make_double4(xy.x, xy.y, p->z, __longlong_as_double((long long)g));
+      }
+      const int m = __popcll(im);
+      scanned_pts += m;
+      // the staging area holds 32 fp64 points: the chunk's in-B points in two halves
+      for (int h = 0; h < m; h += 32) {
+        wave_lds_fence();  // the previous half's reads are done before its slots are rewritten
+        if (nin && slot >= h && slot < h + 32) stage[slot - h] = cur;
+        wave_lds_fence();
+        const int mh = m - h < 32 ? m - h : 32;
+        for (int k = 0; k < mh; k++) {
+          const double4 pt = stage[k];
+          const double dx = pt.x - qx, dy = pt.y - qy, dz = pt.z - qz;
+          const double d2 = dx * dx + dy * dy + dz * dz;
+          if (d2 < best) {
+            second = best;
+            best = d2;
+            bpos = (int32_t)__double_as_longlong(pt.w);
+          } else if (d2 < second) {
+            second = d2;
+          }
+        }
+      }
+    }
+    if (a.dbg && lane == 0) atomicAdd(&a.dbg[4], (unsigned long long)scanned_pts);
+  }
+  if (a.dbg) {
+    const unsigned long long ex = __ballot(cand && !join && !overflow);
+    const unsigned long long cov = __ballot(join && !(best <= u));
+    const unsigned long long nc = __ballot(active && finite_q && !cand);
+    if (lane == 0) {
+      atomicAdd(&a.dbg[2], (unsigned long long)__popcll(ex));
+      atomicAdd(&a.dbg[3], (unsigned long long)__popcll(cov));
+      atomicAdd(&a.dbg[6], (unsigned long long)__popcll(nc));
+      atomicAdd(&a.dbg[7], (unsigned long long)nleaf);
+    }
+  }
+
+  const unsigned long long t_p4 = a.dbg ? __builtin_amdgcn_s_memtime() : 0ull;
+  // Phase 5: certify, write, or queue.
+  bool written = false, to_exact = false, to_lane = false;
+  double d = 0.0;
+  int32_t pos = bpos;
+  if (active) {
+    if (!finite_q) {
+      // NaN: every leaf distance is NaN; inf: the root's distance is inf. Either way the
+      // reference keeps findNearest's default index 0 (octree.cpp:179).
+      pos = a.pos0;
+      d = residual_to(a.pts, pos, qx, qy, qz);
+      written = true;
+    } else if (join && !(best <= u)) {
+      to_lane = true;  // the guess did not cover the nearest point: search this one per lane
+    } else if (join) {
+      written = certified(best, second, a.init_best);
+      to_exact = !written;
+      d = __builtin_sqrt(best);
+    } else {
+      to_lane = true;
+    }
+    if (written) {
+      a.pos_out[i] = pos;
+      a.dist_out[i] = d;
+    }
+  }
+  wave_append(to_exact, i, a.fb_count, a.fb_list);
+  const bool covered = !(join && !(best <= u));
+  wave_append_u(to_lane, i, covered ? u : __builtin_inf(), a.fb_count + 1, a.fb_list2, a.fb_u2);
+  if (a.dbg && lane == 0) {
+    const unsigned long long t_p5 = __builtin_amdgcn_s_memtime();
+    atomicAdd(&a.dbg[16], t_p2 - t_p0);
+    atomicAdd(&a.dbg[17], t_p3 - t_pd);
+    atomicAdd(&a.dbg[20], t_pd - t_p2);
+    atomicAdd(&a.dbg[18], t_p4 - t_p3);
+    atomicAdd(&a.dbg[19], t_p5 - t_p4);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// The ball search: four queries per wave, one 16-lane group (a DPP row) each. The list's queries
+// are latency-bound walks of a few dependent rounds, so four in flight per wave hide four times
+// the latency of one. A group collects, breadth-first from the cell tables of the query's box,
+// every leaf whose box distance s <= u (1 + 2^-47) (a sphere test) and scans their points one per
+// lane. Leaves with s > u (1 + 2^-47) only hold points with fl(d2) > best (1 + 2^-48) (monotone
+// rounding), so nothing in the certificate window is missed. Certification as in the wave search
+// (best <= u and the window test). No usable guess or an overflowing candidate set -> the lane
+// list.
+constexpr int kBallGroups = 4;
+constexpr int kBallGL = 64 / kBallGroups;  // lanes per query
+constexpr int kBallStack = 512;
+constexpr int kBallPoints = 1024;
+constexpr int kBallGStack = kBallStack / kBallGroups;
+constexpr int kBallGPoints = kBallPoints / kBallGroups;
+constexpr int kBallLdsBytes = kBallStack * 4 + kBallPoints * 4;
+
+__global__ void __launch_bounds__(64) k_nn_ball(NNLaunch a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned long long lds_raw[];
+  const int lane = threadIdx.x, g = lane / kBallGL, gl = lane % kBallGL, gbase = g * kBallGL;
+  int32_t* stack = reinterpret_cast<int32_t*>(lds_raw) + g * kBallGStack;
+  int32_t* plist = reinterpret_cast<int32_t*>(lds_raw) + kBallStack + g * kBallGPoints;
+  const unsigned cnt = a.fb_count[1];
+  for (unsigned j0 = blockIdx.x * kBallGroups; j0 < cnt; j0 += gridDim.x * kBallGroups) {
+    const unsigned j = j0 + g;
+    bool live = j < cnt;  // group-uniform
+    int64_t i = 0;
+    double u = 0.0, qx = 0.0, qy = 0.0, qz = 0.0;
+    if (live) {
+      i = a.fb_list2[j];
+      u = a.fb_u2[j];
+      qx = a.x[i];
+      qy = a.y[i];
+      qz = a.z[i];
+      if (!(u <= 0x1p900)) {
+        if (gl == 0) a.fb_list3[atomicAdd(a.fb_count + 2, 1u)] = (int32_t)i;
+        live = false;
+      }
+    }
+    const double thr = u * (1.0 + kFastPrune);
+    int tail = 0, npts = 0;
+    bool overflow = false;
+    wave_lds_fence();
+    {
+      // every point with fl(d2) <= thr lies in the box q +- r (see the wave search's radius)
+      const double amax = __builtin_fmax(__builtin_fabs(qx), __builtin_fmax(__builtin_fabs(qy), __builtin_fabs(qz)));
+      const double r = live ? __builtin_sqrt(thr) * (1.0 + 0x1p-40) + amax * 0x1p-45 : 0.0;
+      if (a.cells) {
+        const int t = cell_starts<kBallGL>(a, qx - r, qy - r, qz - r, qx + r, qy + r, qz + r, gl, gbase, stack);
+        tail = live ? t : 0;
+      } else {
+        if (gl == 0) stack[0] = 0;
+        tail = live ? 1 : 0;
+      }
+    }
+    wave_lds_fence();
+    // LIFO batches of up to 16 nodes per group, sphere test s <= thr on the children
+    while (__ballot(tail > 0) != 0) {
+      const int batch = tail < kBallGL ? tail : kBallGL;
+      const bool has = gl < batch;
+      bool leaf = false;
+      int32_t first = 0;
+      uint32_t meta = 0, kids = 0;
+      if (has) {
+        const NodeRec* rr = a.nodes + stack[tail - batch + gl];
+        const int2 topo = *reinterpret_cast<const int2*>(&rr->first);
+        first = topo.x;
+        meta = (uint32_t)topo.y;
+        leaf = (meta & kLeafBit) != 0;
+        if (!leaf) kids = children_in_ball(rr, meta & 0xffu, qx, qy, qz, thr);
+      }
+      const int lcnt = (has && leaf) ? (int)(meta & ~kLeafBit) : 0;
+      int ltot;
+      const int lincl = row_incl_scan(lcnt, gbase, &ltot);
+      const int lpos = npts + lincl - lcnt;
+      if (lcnt > 0 && lpos + lcnt <= kBallGPoints)
+        for (int c = 0; c < lcnt; c++) plist[lpos + c] = first + c;
+      const int nch = __builtin_popcount(kids);
+      int tot;
+      const int incl = row_incl_scan(nch, gbase, &tot);
+      if (tail > 0) {
+        npts += ltot;
+        tail -= batch;
+        if (npts > kBallGPoints || tail + tot > kBallGStack) {
+          overflow = true;
+          tail = 0;
+        } else {
+          int off = tail + incl - nch;
+          const uint32_t mask = meta & 0xffu;
+          uint32_t kk = kids;
+          while (kk) {
+            const uint32_t o = (uint32_t)__builtin_ctz(kk);
+            kk &= kk - 1u;
+            stack[off++] = first + __builtin_popcount(mask & ((1u << o) - 1u));
+          }
+          tail += tot;
+        }
+      }
+      wave_lds_fence();
+    }
+    if (a.dbg && gl == 0 && live) {
+      atomicAdd(&a.dbg[14], overflow ? 1ull : 0ull);
+      atomicAdd(&a.dbg[15], (unsigned long long)npts);
+    }
+    if (live && overflow && gl == 0) a.fb_list3[atomicAdd(a.fb_count + 2, 1u)] = (int32_t)i;
+    if (overflow) live = false;
+    wave_lds_fence();
+    double best = __builtin_inf(), second = __builtin_inf();
+    int32_t bpos = 0x7fffffff;
+    if (live) {
+      for (int k = gl; k < npts; k += kBallGL) {
+        const int32_t pg = plist[k];
+        const TgtPt* p = a.pts + pg;
+        const double2 xy = *reinterpret_cast<const double2*>(&p->x);
+        const double dx = xy.x - qx, dy = xy.y - qy, dz = p->z - qz;
+        const double d2 = dx * dx + dy * dy + dz * dz;
+        if (d2 < best) {
+          second = best;
+          best = d2;
+          bpos = pg;
+        } else if (d2 < second) {
+          second = d2;
+        }
+      }
+    }
+#pragma unroll
+    for (int o = kBallGL / 2; o >= 1; o >>= 1) {
+      const double ob = __shfl_xor(best, o, kWave);
+      const double os = __shfl_xor(second, o, kWave);
+      const int32_t op = __shfl_xor(bpos, o, kWave);
+      const double lo_ = ob < best ? ob : best;
+      const double hi_ = ob < best ? best : ob;
+      const double ss = os < second ? os : second;
+      second = hi_ < ss ? hi_ : ss;
+      bpos = (ob < best || (ob == best && op < bpos)) ? op : bpos;
+      best = lo_;
+    }
+    if (live && gl == 0) {
+      if (!(best <= u)) {
+        a.fb_list3[atomicAdd(a.fb_count + 2, 1u)] = (int32_t)i;
+      } else if (certified(best, second, a.init_best)) {
+        a.pos_out[i] = bpos;
+        a.dist_out[i] = __builtin_sqrt(best);
+      } else {
+        a.fb_list[atomicAdd(a.fb_count, 1u)] = (int32_t)i;
+      }
+    }
+    wave_lds_fence();
+  }
+}
+
+// The two short lists the ball search leaves, in one launch: thread j < n3 takes lane-list entry
+// j (per-lane certified search; a query it cannot certify gets the reference-order DFS right
+// away, in the same thread), the rest take the exact list (queries the wave or the ball search
+// could not certify). Both lists are complete when this kernel starts; it appends nothing.
+__global__ void __launch_bounds__(64) k_nn_lists(NNLaunch a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned long long lds_stack[];
+  const unsigned n3 = a.fb_count[2], n0 = a.fb_count[0];
+  for (unsigned j = blockIdx.x * blockDim.x + threadIdx.x; j < n3 + n0; j += gridDim.x * blockDim.x) {
+    const bool lane_list = j < n3;
+    const int64_t i = lane_list ? a.fb_list3[j] : a.fb_list[j - n3];
+    const double qx = a.x[i], qy = a.y[i], qz = a.z[i];
+    if (lane_list) {
+      double best = __builtin_inf(), second = __builtin_inf();
+      int32_t bpos = -1;
+      fast_dfs(a, qx, qy, qz, lds_stack + threadIdx.x, blockDim.x, best, second, bpos);
+      if (certified(best, second, a.init_best)) {
+        a.pos_out[i] = bpos;
+        a.dist_out[i] = __builtin_sqrt(best);
+        continue;
+      }
+    }
+    double best_d2 = a.init_best, visits = 0.0, scanned = 0.0;
+    int32_t best = -1;
+    exact_dfs<false>(a, qx, qy, qz, lds_stack + threadIdx.x, blockDim.x, best, best_d2, visits, scanned);
+    a.pos_out[i] = best >= 0 ? best : a.pos0;
+    a.dist_out[i] = best >= 0 ? __builtin_sqrt(best_d2) : residual_to(a.pts, a.pos0, qx, qy, qz);
+  }
+}
+
+inline unsigned grid_for(int64_t n, int bs) { return (unsigned)((n + bs - 1) / bs); }
+
+}  // namespace
+
+int nn_block_threads(int levels) {
+  // LDS stack of the per-thread kernels: levels x threads x 8 B. Keep <= 64 KiB per block.
+  if (levels <= 32) return 256;
+  if (levels <= 64) return 128;
+  return 64;
+}
+
+hipError_t launch_nn(const NNLaunch& a, hipStream_t s) {
+  if (a.n <= 0) return hipSuccess;
+  const int levels = a.levels < 1 ? 1 : a.levels;
+  const int bs = nn_block_threads(levels);
+  size_t shmem = (size_t)levels * bs * sizeof(unsigned long long);
+  if (shmem < 1024) shmem = 1024;  // also hosts the block reduction
+  const unsigned grid = grid_for(a.n, bs);
+  if (a.search == ICP_SEARCH_REFERENCE || a.count) {
+    if (a.apply) {
+      if (a.count) hipLaunchKernelGGL((k_nn_ref<true, true>), dim3(grid), dim3(bs), shmem, s, a);
+      else hipLaunchKernelGGL((k_nn_ref<true, false>), dim3(grid), dim3(bs), shmem, s, a);
+    } else {
+      if (a.count) hipLaunchKernelGGL((k_nn_ref<false, true>), dim3(grid), dim3(bs), shmem, s, a);
+      else hipLaunchKernelGGL((k_nn_ref<false, false>), dim3(grid), dim3(bs), shmem, s, a);
+    }
+    if (a.ev_fast_done) (void)hipEventRecord(a.ev_fast_done, s);
+    return hipGetLastError();
+  }
+  // wave search -> ball search -> per-lane search / exact DFS
+  const unsigned wgrid = grid_for(a.n, 256);
+  const size_t wshm = (size_t)(256 / 64) * kWaveLds;
+  if (a.apply) hipLaunchKernelGGL((k_nn_wave<true>), dim3(wgrid), dim3(256), wshm, s, a);
+  else hipLaunchKernelGGL((k_nn_wave<false>), dim3(wgrid), dim3(256), wshm, s, a);
+  if (a.ev_fast_done) (void)hipEventRecord(a.ev_fast_done, s);
+  // the lists are short (usually empty after the first iteration): small grids of 64-thread
+  // blocks, grid-stride over the list
+  const int64_t bq = (a.n + kBallGroups - 1) / kBallGroups;
+  hipLaunchKernelGGL(k_nn_ball, dim3((unsigned)(bq < 8192 ? bq : 8192)), dim3(64), kBallLdsBytes, s, a);
+  const int64_t lq = (a.n + 63) / 64;
+  size_t lshm = (size_t)levels * 64 * sizeof(unsigned long long);
+  if (lshm < 1024) lshm = 1024;
+  hipLaunchKernelGGL(k_nn_lists, dim3((unsigned)(lq < 1024 ? lq : 1024)), dim3(64), lshm, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace icp

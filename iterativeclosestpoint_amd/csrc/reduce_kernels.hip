@@ -1,0 +1,425 @@
+// reduce_kernels.hip — gfx950 reductions of one ICP iteration after the correspondence search.
+//
+//  k_moments        residual moments of fixed 4096-query parts (icpengine.cpp:235-245)
+//  k_cull_cov       3-sigma cull (icpengine.cpp:263-278) + valid-pair centroid and cross-covariance
+//                   sums (icpengine.cpp:76-90, computeBestFitTransform's H = AA * BB^T)
+//  k_tree_merge, k_merge_*_last   fixed-shape merge trees of the part sums (deterministic)
+//  k_finalize_*     rank-ordered merge of the gathered per-rank records (multi-GPU)
+//  publish          the last kernel of an iteration stores the finished record into pinned host
+//                   memory, sequence word last: the host's only wait of the iteration
+//
+// fp64, -ffp-contract=off.
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+
+#include "kernels.h"
+#include "nn_device.h"
+
+namespace icp {
+
+namespace {
+
+using namespace dev;
+
+// Rank-level reductions as shifted plain sums. A part holds sums of values shifted by a constant
+// of the iteration (query 0's residual, source point and match), so the sums stay at the spread
+// of the data, not at its offset (LAS-sized coordinates), and the merge tree is plain additions
+// in a fixed order: deterministic and cheap. The last level turns them into (count, mean, M2)
+// and (count, means, co-moment) records, which ranks merge with the Chan formulas (icp_common.h).
+struct MomSums {
+  double n, s1, s2, dmin, dmax, nbad, pad0, pad1;  // s1 = sum (d - c), s2 = sum (d - c)^2
+};
+struct CovSums {
+  double n, sum_d2, sa[3], sb[3], sab[9], pad[3];  // sa = sum (a - s), sb = sum (b - t), sab = sum (a - s)(b - t)^T
+};
+static_assert(sizeof(MomSums) == sizeof(Moments) && sizeof(CovSums) == sizeof(CovMoments), "part buffers");
+
+__device__ __forceinline__ MomSums momsum_identity() {
+  MomSums m;
+  m.n = m.s1 = m.s2 = m.nbad = m.pad0 = m.pad1 = 0.0;
+  m.dmin = 1.7976931348623157e308;
+  m.dmax = 0.0;
+  return m;
+}
+__device__ MomSums momsum_merge(const MomSums& a, const MomSums& b) {
+  MomSums r;
+  r.n = a.n + b.n;
+  r.s1 = a.s1 + b.s1;
+  r.s2 = a.s2 + b.s2;
+  r.dmin = b.dmin < a.dmin ? b.dmin : a.dmin;
+  r.dmax = b.dmax > a.dmax ? b.dmax : a.dmax;
+  r.nbad = a.nbad + b.nbad;
+  r.pad0 = r.pad1 = 0.0;
+  return r;
+}
+__device__ __forceinline__ CovSums covsum_identity() {
+  CovSums c;
+  c.n = c.sum_d2 = 0.0;
+  for (int k = 0; k < 3; k++) c.sa[k] = c.sb[k] = c.pad[k] = 0.0;
+  for (int k = 0; k < 9; k++) c.sab[k] = 0.0;
+  return c;
+}
+__device__ CovSums covsum_merge(const CovSums& a, const CovSums& b) {
+  CovSums r;
+  r.n = a.n + b.n;
+  r.sum_d2 = a.sum_d2 + b.sum_d2;
+  for (int k = 0; k < 3; k++) {
+    r.sa[k] = a.sa[k] + b.sa[k];
+    r.sb[k] = a.sb[k] + b.sb[k];
+    r.pad[k] = 0.0;
+  }
+  for (int k = 0; k < 9; k++) r.sab[k] = a.sab[k] + b.sab[k];
+  return r;
+}
+
+// The shifts of this iteration: query 0's residual, its source point and its match (a function of
+// this iteration's data only, so equal inputs give equal bits; every block and the last level
+// compute the same values). Any finite shift is correct; one inside the data keeps the sums at
+// the scale of the data's spread.
+__device__ __forceinline__ double moment_shift(const double* dist, int64_t n) {
+  const double d0 = n > 0 ? dist[0] : 0.0;
+  return __builtin_isfinite(d0) ? d0 : 0.0;
+}
+__device__ __forceinline__ void cov_shift(const double* x, const double* y, const double* z, const int32_t* pos,
+                                          const TgtPt* pts, int64_t n, double sh[6]) {
+  for (int k = 0; k < 6; k++) sh[k] = 0.0;
+  if (n <= 0) return;
+  const TgtPt p = pts[pos[0]];
+  const double v[6] = {x[0], y[0], z[0], p.x, p.y, p.z};
+  for (int k = 0; k < 6; k++) sh[k] = __builtin_isfinite(v[k]) ? v[k] : 0.0;
+}
+
+// Residual moments of the rank's queries in fixed parts of kMomPart queries, once every search
+// kernel has written its residuals: deterministic whatever order the queries were settled in.
+// Thread t of block p holds queries p kMomPart + t + 256 e (e < kMomPer, coalesced).
+constexpr int kMomPer = 16;
+constexpr int kMomPart = 256 * kMomPer;
+
+__global__ void __launch_bounds__(256) k_moments(const double* __restrict__ dist, int64_t n, MomSums* part) {
+  __shared__ double red[4 * 4];
+  const double c = moment_shift(dist, n);
+  const int64_t b0 = (int64_t)blockIdx.x * kMomPart + threadIdx.x;
+  double v[4] = {0.0, 0.0, 0.0, 0.0};  // count, sum (d - c), sum (d - c)^2, non-finite
+  double mn = 1.7976931348623157e308, mx = 0.0;
+#pragma unroll
+  for (int e = 0; e < kMomPer; e++) {
+    const int64_t i = b0 + 256 * e;
+    const bool act = i < n;
+    const double d = act ? dist[i] : 0.0;
+    const double dv = act ? d - c : 0.0;
+    v[0] += act ? 1.0 : 0.0;
+    v[1] += dv;
+    v[2] += dv * dv;
+    const bool fin = act && __builtin_isfinite(d);
+    v[3] += (act && !fin) ? 1.0 : 0.0;
+    mn = fin && d < mn ? d : mn;
+    mx = fin && d > mx ? d : mx;
+  }
+  block_sum<4>(v, red);
+  block_minmax(mn, mx, red);
+  if (threadIdx.x == 0) {
+    MomSums m;
+    m.n = v[0];
+    m.s1 = v[1];
+    m.s2 = v[2];
+    m.dmin = mn;
+    m.dmax = mx;
+    m.nbad = v[3];
+    m.pad0 = m.pad1 = 0.0;
+    part[blockIdx.x] = m;
+  }
+}
+
+// Fixed-shape merges of part sums, deterministic: the same n always gives the same merge tree.
+// Inner levels: block b merges items [256 b, 256 b + 256), one per thread, pairwise in LDS. Last
+// level: one block, up to 4096 items: thread t folds items t + 256 k (k < 16) in order, then the
+// block's pairwise tree.
+constexpr int kLastSpan = 4096;
+
+template <typename T, T (*Merge)(const T&, const T&), T (*Identity)()>
+__device__ __forceinline__ T block_tree(T v, T* sm) {
+  const int t = threadIdx.x;
+  sm[t] = v;
+  __syncthreads();
+  for (int s = 1; s < 256; s <<= 1) {
+    if ((t & (2 * s - 1)) == 0) sm[t] = Merge(sm[t], sm[t + s]);
+    __syncthreads();
+  }
+  return sm[0];
+}
+
+template <typename T, T (*Merge)(const T&, const T&), T (*Identity)()>
+__device__ __forceinline__ T block_tree_last(const T* in, int64_t n, T* sm) {
+  // No early exit: block_tree's barriers must be reached by every thread in uniform control flow.
+  T acc = Identity();
+#pragma unroll 4
+  for (int k = 0; k < 16; k++) {
+    const int64_t g = (int64_t)threadIdx.x + 256 * k;
+    if (g < n) acc = Merge(acc, in[g]);
+  }
+  return block_tree<T, Merge, Identity>(acc, sm);
+}
+
+template <typename T, T (*Merge)(const T&, const T&), T (*Identity)()>
+__global__ void __launch_bounds__(256) k_tree_merge(const T* in, int64_t n, T* out) {
+  __shared__ T sm[256];
+  const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const T r = block_tree<T, Merge, Identity>(g < n ? in[g] : Identity(), sm);
+  if (threadIdx.x == 0) out[blockIdx.x] = r;
+}
+
+// mean = sum/row; std = sqrt(variance/row) (icpengine.cpp:235-245); threshold rule of the caller
+__device__ void finalize_moments(IterDev* it, const Moments& g, const MomentsFinalize& f) {
+  it->m_global = g;
+  const double mean = g.mean;
+  const double sd = __builtin_sqrt(g.m2 / g.n);
+  it->mean = mean;
+  it->sd = sd;
+  it->thr = cull_threshold(mean, sd, f.k_sigma, f.iter, f.engine_rules);
+}
+
+// Last level of the rank's moments: the summed part -> (count, mean, M2) in it->m_local; with fin
+// (one rank, no communicator) also the statistics.
+__global__ void __launch_bounds__(256) k_merge_moments_last(const MomSums* in, int64_t n, const double* dist,
+                                                           int64_t nq, IterDev* it, MomentsFinalize fin, int finalize) {
+  __shared__ MomSums sm[256];
+  const MomSums r = block_tree_last<MomSums, momsum_merge, momsum_identity>(in, n, sm);
+  if (threadIdx.x == 0) {
+    const double c = moment_shift(dist, nq);
+    Moments m = moments_identity();
+    if (r.n > 0.0) {
+      m.n = r.n;
+      m.mean = c + r.s1 / r.n;
+      const double m2 = r.s2 - r.s1 * (r.s1 / r.n);
+      m.m2 = m2 < 0.0 ? 0.0 : m2;  // rounding only; NaN propagates
+      m.dmin = r.dmin;
+      m.dmax = r.dmax;
+    }
+    m.nbad = r.nbad;
+    it->m_local = m;
+    if (finalize) finalize_moments(it, m, fin);
+  }
+}
+
+__global__ void k_finalize_moments(const Moments* gathered, int nranks, IterDev* it, MomentsFinalize fin) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  Moments g = gathered[0];
+  for (int r = 1; r < nranks; r++) g = moments_merge(g, gathered[r]);  // rank order: same bits everywhere
+  finalize_moments(it, g, fin);
+}
+
+// The iteration's record goes straight into the caller's pinned host buffer (no copy engine or
+// blit launch on the critical path): the block copies the device record to LDS, thread 0
+// completes it, the block stores it with system-scope relaxed stores, every thread waits for its
+// stores to be acknowledged, then thread 0 stores the sequence word. No system-scope release
+// fence: it would write back the whole L2, which the search has just dirtied with megabytes. The
+// list sizes ride along (pad[0..2]) and are reset for the next search.
+__device__ void finalize_cov_publish(IterDev* it, const CovMoments& g, IterPublish pub, IterDev* rec) {
+  constexpr int kWords = (int)(sizeof(IterDev) / sizeof(double)) - 1;  // all but pad[3], the flag
+  static_assert(offsetof(IterDev, pad) + 3 * sizeof(double) == kWords * sizeof(double), "flag is the last word");
+  double* rw = reinterpret_cast<double*>(rec);
+  const double* iw = reinterpret_cast<const double*>(it);
+  for (int k = threadIdx.x; k < kWords + 1; k += blockDim.x) rw[k] = iw[k];  // the device record, in parallel
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    rec->c_global = g;
+    rec->rmse = (g.n > 0) ? __builtin_sqrt(g.sum_d2 / g.n) : 0.0;  // icpengine.cpp:274-278
+    for (int k = 0; k < 3; k++) {
+      rec->pad[k] = (double)pub.lists[k];
+      pub.lists[k] = 0u;
+    }
+    it->c_global = rec->c_global;
+    it->rmse = rec->rmse;
+  }
+  __syncthreads();
+  double* dst = reinterpret_cast<double*>(pub.host);
+  for (int k = threadIdx.x; k < kWords; k += blockDim.x)
+    __hip_atomic_store(dst + k, rw[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(&pub.host->pad[3], pub.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ void __launch_bounds__(256) k_merge_cov_last(const CovSums* in, int64_t n, CullLaunch cl, IterDev* it,
+                                                       IterPublish pub, int finalize) {
+  __shared__ CovSums sm[256];
+  __shared__ IterDev rec;
+  const CovSums r = block_tree_last<CovSums, covsum_merge, covsum_identity>(in, n, sm);
+  __shared__ CovMoments res;
+  if (threadIdx.x == 0) {
+    double sh[6];
+    cov_shift(cl.x, cl.y, cl.z, cl.pos, cl.pts, cl.n, sh);
+    CovMoments m = cov_identity();
+    if (r.n > 0.0) {
+      m.n = r.n;
+      m.sum_d2 = r.sum_d2;
+      double da[3], db[3];
+      for (int k = 0; k < 3; k++) {
+        da[k] = r.sa[k] / r.n;
+        db[k] = r.sb[k] / r.n;
+        m.ma[k] = sh[k] + da[k];
+        m.mb[k] = sh[3 + k] + db[k];
+      }
+      for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) m.c[3 * i + j] = r.sab[3 * i + j] - r.n * (da[i] * db[j]);
+    }
+    it->c_local = m;
+    res = m;
+  }
+  if (!finalize) return;
+  __syncthreads();
+  finalize_cov_publish(it, res, pub, &rec);
+}
+
+__global__ void __launch_bounds__(64) k_finalize_cov(const CovMoments* gathered, int nranks, IterDev* it,
+                                                     IterPublish pub) {
+  __shared__ IterDev rec;
+  CovMoments g = gathered[0];
+  for (int r = 1; r < nranks; r++) g = cov_merge(g, gathered[r]);  // rank order
+  finalize_cov_publish(it, g, pub, &rec);
+}
+
+// 3-sigma cull + covariance sums. One thread per 4 queries (1024 per block). A thread first
+// issues all its streamed loads (d, pos, x, y, z of its 4 queries), then all 4 match gathers (a
+// culled query gathers point 0, always valid), then accumulates in query order: two dependent
+// memory round trips instead of three.
+constexpr int kCullPer = 4;
+
+__global__ void __launch_bounds__(256) k_cull_cov(CullLaunch a) {
+  __shared__ double red[4 * 17];
+  const double thr = a.it->thr;
+  double sh[6];
+  cov_shift(a.x, a.y, a.z, a.pos, a.pts, a.n, sh);
+  const int64_t base = (int64_t)blockIdx.x * (256 * kCullPer) + threadIdx.x;
+  // count, sum d^2, sum (a - s), sum (b - t), sum (a - s)(b - t)^T over the valid pairs
+  double v[17];
+#pragma unroll
+  for (int k = 0; k < 17; k++) v[k] = 0.0;
+  double dq[kCullPer], qx[kCullPer], qy[kCullPer], qz[kCullPer];
+  int32_t pq[kCullPer];
+#pragma unroll
+  for (int e = 0; e < kCullPer; e++) {
+    const int64_t i = base + e * 256;
+    const bool in = i < a.n;
+    dq[e] = in ? a.dist[i] : __builtin_nan("");  // NaN <= thr is false: not a valid pair
+    pq[e] = in ? a.pos[i] : 0;
+    qx[e] = in ? a.x[i] : 0.0;
+    qy[e] = in ? a.y[i] : 0.0;
+    qz[e] = in ? a.z[i] : 0.0;
+  }
+  double mx[kCullPer], my[kCullPer], mz[kCullPer];
+#pragma unroll
+  for (int e = 0; e < kCullPer; e++) {
+    const TgtPt* p = a.pts + (dq[e] <= thr ? pq[e] : 0);
+    const double2 pxy = *reinterpret_cast<const double2*>(&p->x);
+    mx[e] = pxy.x;
+    my[e] = pxy.y;
+    mz[e] = p->z;
+  }
+#pragma unroll
+  for (int e = 0; e < kCullPer; e++) {
+    const double d = dq[e];
+    if (d <= thr) {  // icpengine.cpp:265
+      const double da[3] = {qx[e] - sh[0], qy[e] - sh[1], qz[e] - sh[2]};
+      const double db[3] = {mx[e] - sh[3], my[e] - sh[4], mz[e] - sh[5]};
+      v[0] += 1.0;
+      v[1] += d * d;
+#pragma unroll
+      for (int r = 0; r < 3; r++) {
+        v[2 + r] += da[r];
+        v[5 + r] += db[r];
+#pragma unroll
+        for (int c = 0; c < 3; c++) v[8 + 3 * r + c] += da[r] * db[c];
+      }
+    }
+  }
+  block_sum<17>(v, red);
+  if (threadIdx.x == 0) {
+    CovSums m;
+    m.n = v[0];
+    m.sum_d2 = v[1];
+    for (int k = 0; k < 3; k++) {
+      m.sa[k] = v[2 + k];
+      m.sb[k] = v[5 + k];
+      m.pad[k] = 0.0;
+    }
+    for (int k = 0; k < 9; k++) m.sab[k] = v[8 + k];
+    reinterpret_cast<CovSums*>(a.part)[blockIdx.x] = m;
+  }
+}
+
+template <typename T, T (*Merge)(const T&, const T&), T (*Identity)()>
+const T* merge_to_last_span(const T* part, int64_t* nparts, hipStream_t s) {
+  // part -> scratch levels (right behind the partials) until the last block's span is left
+  const T* cur = part;
+  T* next = const_cast<T*>(part) + *nparts;
+  int64_t cn = *nparts;
+  while (cn > kLastSpan) {
+    const int64_t nb = (cn + 255) / 256;
+    hipLaunchKernelGGL((k_tree_merge<T, Merge, Identity>), dim3((unsigned)nb), dim3(256), 0, s, cur, cn, next);
+    cur = next;
+    next += nb;
+    cn = nb;
+  }
+  *nparts = cn;
+  return cur;
+}
+
+}  // namespace
+
+// Partial buffers hold the block partials followed by the merge scratch (merge_scratch_entries).
+int64_t merge_scratch_entries(int64_t nparts) {
+  int64_t total = 0;
+  for (int64_t cn = nparts; cn > kLastSpan; cn = (cn + 255) / 256) total += (cn + 255) / 256;
+  return total + 1;
+}
+
+int64_t moments_num_parts(int64_t n) { return (n + kMomPart - 1) / kMomPart; }
+
+hipError_t launch_moments(const double* dist, int64_t n, Moments* part, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_moments, dim3((unsigned)moments_num_parts(n)), dim3(256), 0, s, dist, n,
+                     reinterpret_cast<MomSums*>(part));
+  return hipGetLastError();
+}
+
+hipError_t launch_merge_moments(const Moments* part, int64_t nparts, const double* dist, int64_t nq, IterDev* it,
+                                const MomentsFinalize* fin, hipStream_t s) {
+  const MomSums* cur = merge_to_last_span<MomSums, momsum_merge, momsum_identity>(
+      reinterpret_cast<const MomSums*>(part), &nparts, s);
+  hipLaunchKernelGGL(k_merge_moments_last, dim3(1), dim3(256), 0, s, cur, nparts, dist, nq, it,
+                     fin ? *fin : MomentsFinalize{0.0, 0, 0}, fin ? 1 : 0);
+  return hipGetLastError();
+}
+
+hipError_t launch_finalize_moments(const Moments* gathered, int nranks, IterDev* it, MomentsFinalize fin,
+                                   hipStream_t s) {
+  hipLaunchKernelGGL(k_finalize_moments, dim3(1), dim3(64), 0, s, gathered, nranks, it, fin);
+  return hipGetLastError();
+}
+
+int64_t cull_num_blocks(int64_t n) { return (n + 256 * kCullPer - 1) / (256 * kCullPer); }
+
+hipError_t launch_cull_cov(const CullLaunch& a, hipStream_t s) {
+  if (a.n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_cull_cov, dim3((unsigned)cull_num_blocks(a.n)), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_merge_cov(const CovMoments* part, int64_t nparts, const CullLaunch& cl, IterDev* it,
+                            const IterPublish* pub, hipStream_t s) {
+  const CovSums* cur = merge_to_last_span<CovSums, covsum_merge, covsum_identity>(
+      reinterpret_cast<const CovSums*>(part), &nparts, s);
+  hipLaunchKernelGGL(k_merge_cov_last, dim3(1), dim3(256), 0, s, cur, nparts, cl, it,
+                     pub ? *pub : IterPublish{nullptr, nullptr, 0.0}, pub ? 1 : 0);
+  return hipGetLastError();
+}
+
+hipError_t launch_finalize_cov(const CovMoments* gathered, int nranks, IterDev* it, IterPublish pub,
+                               hipStream_t s) {
+  hipLaunchKernelGGL(k_finalize_cov, dim3(1), dim3(64), 0, s, gathered, nranks, it, pub);
+  return hipGetLastError();
+}
+
+}  // namespace icp

@@ -1,0 +1,85 @@
+// util_kernels.hip — layout kernels around the search: the standalone transform
+// (icpengine.cpp:345-346, src = T * src in Eigen's order) and the AoS <-> SoA conversions at the
+// boundary (caller's AoS xyz, pointcloud.h:12-23 / the kd-ordered SoA source in HBM).
+#include <hip/hip_runtime.h>
+
+#include "kernels.h"
+
+namespace icp {
+
+namespace {
+
+struct T12 {
+  double v[12];
+};
+
+__global__ void k_apply(T12 T, double* x, double* y, double* z, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const double qx = x[i], qy = y[i], qz = z[i];
+  x[i] = ((T.v[0] * qx + T.v[1] * qy) + T.v[2] * qz) + T.v[3];
+  y[i] = ((T.v[4] * qx + T.v[5] * qy) + T.v[6] * qz) + T.v[7];
+  z[i] = ((T.v[8] * qx + T.v[9] * qy) + T.v[10] * qz) + T.v[11];
+}
+
+__global__ void k_scatter_aos(const int32_t* perm, const double* x, const double* y, const double* z,
+                              double* aos, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t j = perm ? perm[i] : i;
+  aos[3 * j] = x[i];
+  aos[3 * j + 1] = y[i];
+  aos[3 * j + 2] = z[i];
+}
+
+__global__ void k_scatter_corr(const int32_t* perm, const int32_t* pos, const TgtPt* pts, int32_t* idx_out,
+                               const double* dist_in, double* dist_out, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t j = perm ? perm[i] : i;
+  if (idx_out) idx_out[j] = pts[pos[i]].orig;
+  if (dist_out) dist_out[j] = dist_in[i];
+}
+
+__global__ void k_deinterleave(const double* aos, double* x, double* y, double* z, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  x[i] = aos[3 * i];
+  y[i] = aos[3 * i + 1];
+  z[i] = aos[3 * i + 2];
+}
+
+inline unsigned grid_for(int64_t n, int bs) { return (unsigned)((n + bs - 1) / bs); }
+
+}  // namespace
+
+hipError_t launch_apply(const double T[12], double* x, double* y, double* z, int64_t n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  T12 t;
+  for (int k = 0; k < 12; k++) t.v[k] = T[k];
+  hipLaunchKernelGGL(k_apply, dim3(grid_for(n, 256)), dim3(256), 0, s, t, x, y, z, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_scatter_aos(const int32_t* perm, const double* x, const double* y, const double* z, double* aos,
+                              int64_t n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_scatter_aos, dim3(grid_for(n, 256)), dim3(256), 0, s, perm, x, y, z, aos, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_scatter_corr(const int32_t* perm, const int32_t* pos, const TgtPt* pts, int32_t* idx_out,
+                               const double* dist_in, double* dist_out, int64_t n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_scatter_corr, dim3(grid_for(n, 256)), dim3(256), 0, s, perm, pos, pts, idx_out, dist_in,
+                     dist_out, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_deinterleave(const double* aos, double* x, double* y, double* z, int64_t n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_deinterleave, dim3(grid_for(n, 256)), dim3(256), 0, s, aos, x, y, z, n);
+  return hipGetLastError();
+}
+
+}  // namespace icp

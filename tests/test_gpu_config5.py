@@ -18,7 +18,6 @@ N = 50_000_000
 
 
 def test_config5_50m(icp, oracle):
-    import os
     import time
     t0 = time.time()
     tgt, src, _ = icp.synth_pair(N)
@@ -49,18 +48,10 @@ def test_config5_50m(icp, oracle):
     print(f"oracle sample checked at {time.time() - t0:.0f} s", flush=True)
 
     # the same iteration with the fp64 scan: identical correspondences
-    old = os.environ.get("ICP_SCAN32")
-    os.environ["ICP_SCAN32"] = "0"
-    try:
-        with icp.Context(0) as ctx:
-            ctx.set_target(tgt, 10, 20, icp.RULES_ENGINE)
-            ctx.set_source(moved)
-            ctx.iterate(None, 0, icp.RULES_ENGINE, 3.0)
-            idx64, d64 = ctx.get_correspondences()
-    finally:
-        if old is None:
-            os.environ.pop("ICP_SCAN32", None)
-        else:
-            os.environ["ICP_SCAN32"] = old
+    with icp.Context(0, {"scan32": 0}) as ctx:
+        ctx.set_target(tgt, 10, 20, icp.RULES_ENGINE)
+        ctx.set_source(moved)
+        ctx.iterate(None, 0, icp.RULES_ENGINE, 3.0)
+        idx64, d64 = ctx.get_correspondences()
     np.testing.assert_array_equal(idx64, idx)
     np.testing.assert_array_equal(d64, d)

@@ -80,6 +80,7 @@ def _worker(rank, world, port, q):
 
 @pytest.mark.parametrize("world", [2, 3])
 def test_host_exchange_ranks_match_one_rank(icp, world):
+    pytest.importorskip("torch")
     import torch.multiprocessing as mp
 
     ctx_mp = mp.get_context("spawn")
@@ -88,9 +89,17 @@ def test_host_exchange_ranks_match_one_rank(icp, world):
     procs = [ctx_mp.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    results = sorted((q.get(timeout=100) for _ in range(world)), key=lambda r: r[0])
-    for p in procs:
-        p.join(timeout=30)
+    try:
+        results = sorted((q.get(timeout=100) for _ in range(world)), key=lambda r: r[0])
+        for p in procs:
+            p.join(timeout=30)
+    finally:
+        # a rank that died without reporting leaves its peers blocked in the gloo all-gather:
+        # end every process still alive so none holds the GPU past the test
+        for p in procs:
+            if p.is_alive():
+                p.kill()
+                p.join(timeout=10)
     for r in results:
         assert r[4] is None, f"rank {r[0]} failed: {r[4]}"
     assert all(p.exitcode == 0 for p in procs)
@@ -119,3 +128,34 @@ def test_host_exchange_ranks_match_one_rank(icp, world):
     for _, rows, idx0, _, _ in results:
         assert np.array_equal(idx0, ref_idx0[rows])
     assert sum(len(r[1]) for r in results) == N
+
+
+def test_rccl_one_rank_communicator_matches_plain(icp):
+    """The RCCL transport on the one GPU a box has: a communicator of one rank
+    (icp_hip_get_unique_id + icp_hip_comm_init(ctx, 1, 0, id)) makes every iteration run the
+    multi-rank path — ncclAllGather of the Moments and CovMoments records on the compute stream,
+    the rank-order device merges k_finalize_moments / k_finalize_cov, the publish from
+    k_finalize_cov. With one record the rank-order merge is the identity, so every statistic,
+    transform and correspondence equals the communicator-free run's bit for bit."""
+    tgt, src, _ = icp.synth_pair(N, yaw_deg=3.0)
+
+    def run(rccl: bool):
+        with icp.Context(0) as ctx:
+            ctx.set_target(tgt, 10, 20, icp.RULES_ENGINE)
+            ctx.set_source(src)
+            if rccl:
+                ctx.comm_init(1, 0, icp.Context.unique_id())
+            params = icp.params_default(max_iterations=ITERS + 1, tolerance=1e-6, flags=icp.FLAG_NO_EARLY_STOP)
+            sess = ctx.session(params)
+            recs = _records(sess, ITERS)
+            idx, d = ctx.get_correspondences()
+            T = sess.transform().copy()
+            sess.close()
+        return recs, idx, d, T
+
+    a, ia, da, Ta = run(True)
+    b, ib, db, Tb = run(False)
+    for x, y in zip(a, b):
+        assert x[:5] == y[:5] and np.array_equal(x[5], y[5])
+    assert np.array_equal(Ta, Tb)
+    assert np.array_equal(ia, ib) and np.array_equal(da, db)

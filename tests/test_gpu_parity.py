@@ -179,37 +179,29 @@ def test_empty_inputs_rejected(icp):
 
 
 def test_kernel_variants_agree(icp, oracle):
-    """The certified fast search (default) and the literal reference-order kernels agree bit for
-    bit, including on inputs full of exact ties (lattice) where the fallback does the work."""
-    import os
+    """The certified wave search (default) and the literal reference-order kernel agree bit for
+    bit, including on inputs full of exact ties (lattice) where the exact DFS does the work."""
     rng = np.random.default_rng(9)
     tgt = rng.normal(size=(200000, 3)) * [5, 5, 1]
     q = np.concatenate([rng.normal(size=(100000, 3)) * [6, 6, 1.2], tgt[:2000]])
     lat = np.stack(np.meshgrid(np.arange(40), np.arange(40), np.arange(10), indexing="ij"), -1).reshape(-1, 3) * 0.5
     lq = np.concatenate([lat[rng.integers(0, len(lat), 5000)] + 0.25, rng.uniform(-1, 21, size=(5000, 3))])
     outs = {}
-    old = os.environ.get("ICP_NN_VARIANT")
-    try:
-        for v in ("1", "2", "3", "4"):
-            os.environ["ICP_NN_VARIANT"] = v
-            with icp.Context(0) as ctx:
-                ctx.set_target(tgt, 10, 20, icp.RULES_ENGINE)
-                a = ctx.nn(q)
-                ctx.set_target(lat.astype(float), 10, 20, icp.RULES_CLI)
-                b = ctx.nn(lq)
-            outs[v] = (a, b)
-    finally:
-        if old is None:
-            os.environ.pop("ICP_NN_VARIANT", None)
-        else:
-            os.environ["ICP_NN_VARIANT"] = old
-    for v in ("2", "3", "4"):
+    for name, cfg in [("reference", {"search": icp.SEARCH_REFERENCE}), ("certified", {}),
+                      ("certified_fp64", {"scan32": 0}), ("certified_root", {"cell_starts": 0})]:
+        with icp.Context(0, cfg) as ctx:
+            ctx.set_target(tgt, 10, 20, icp.RULES_ENGINE)
+            a = ctx.nn(q)
+            ctx.set_target(lat.astype(float), 10, 20, icp.RULES_CLI)
+            b = ctx.nn(lq)
+        outs[name] = (a, b)
+    for name in outs:
         for k in range(2):
-            np.testing.assert_array_equal(outs[v][k][0], outs["1"][k][0])
-            np.testing.assert_array_equal(outs[v][k][1], outs["1"][k][1])
+            np.testing.assert_array_equal(outs[name][k][0], outs["reference"][k][0])
+            np.testing.assert_array_equal(outs[name][k][1], outs["reference"][k][1])
     oidx, _ = oracle.OracleTree(lat.astype(float)).nn(lq, init_best=1e20)
-    np.testing.assert_array_equal(outs["3"][1][0], oidx)
-    np.testing.assert_array_equal(outs["4"][1][0], oidx)
+    np.testing.assert_array_equal(outs["reference"][1][0], oidx)
+    np.testing.assert_array_equal(outs["certified"][1][0], oidx)
 
 
 def test_fallback_share_small_on_scans(icp, gpu_ctx):
@@ -220,33 +212,21 @@ def test_fallback_share_small_on_scans(icp, gpu_ctx):
     assert st.n_fallback <= 0.001 * len(src)
 
 
-def _with_env(env: dict, fn):
-    import os
-    old = {k: os.environ.get(k) for k in env}
-    try:
-        os.environ.update(env)
-        return fn()
-    finally:
-        for k, v in old.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
-
-
-@pytest.mark.parametrize("n,env", [(300_000, {"ICP_SCAN32": "0"}), (1_000_000, {"ICP_SCAN32": "0"}),
-                                   (1_000_000, {"ICP_LCA": "0"}), (300_000, {"ICP_SCAN32": "0", "ICP_LCA": "0"}),
-                                   (1_000_000, {"ICP_CELLS": "0"}), (300_000, {"ICP_CELLS": "0", "ICP_LCA": "0"}),
-                                   (1_000_000, {"ICP_XCD": "1"}), (1_000_000, {"ICP_BALL_GROUPS": "1"})])
-def test_scan32_matches_fp64_scan(icp, n, env):
-    """The fp32 filter scan of the wave search (fp64 winner + rigorous lower bound certificate)
-    returns exactly the fp64 scan's correspondences and residuals, iteration after iteration of
-    the real loop (previous-residual guesses, fused transform)."""
+@pytest.mark.parametrize("n,cfg", [(300_000, {"scan32": 0}), (1_000_000, {"scan32": 0}),
+                                   (1_000_000, {"cell_starts": 0}),
+                                   (300_000, {"cell_starts": 0, "scan32": 0}),
+                                   (1_000_000, {"join_factor": 1e6}),
+                                   (300_000, {"octree_builder": 1})])
+def test_scan32_matches_fp64_scan(icp, n, cfg):
+    """Every configuration of the certified search (fp32 filter scan vs fp64 scan, cell-table
+    starts vs root descent, join rule, host-built octree) returns exactly the default's
+    correspondences and residuals, iteration after iteration of the real loop (previous-residual
+    guesses, fused transform)."""
     tgt, src, _ = icp.synth_pair(n)
 
-    def run():
+    def run(conf):
         out = []
-        with icp.Context(0) as ctx:
+        with icp.Context(0, conf) as ctx:
             ctx.set_target(tgt, 10, 20, icp.RULES_ENGINE)
             ctx.set_source(src)
             T = None
@@ -256,13 +236,13 @@ def test_scan32_matches_fp64_scan(icp, n, env):
                 T = icp.best_fit_from_stats(st)
         return out
 
-    a = run()
-    b = _with_env(env, run)
+    a = run(None)
+    b = run(cfg)
     for (ia, da, fa, ba), (ib, db, fb, bb) in zip(a, b):
         np.testing.assert_array_equal(ia, ib)
         np.testing.assert_array_equal(da, db)
         assert fa == fb
-        if "ICP_CELLS" not in env:  # the same candidate sets (cell starts change which waves overflow)
+        if set(cfg) <= {"scan32", "octree_builder"}:  # the same candidate sets
             assert ba == bb
 
 
@@ -282,7 +262,7 @@ def test_scan32_ties_and_self_queries(icp, oracle, golden_nn):
                 ctx.iterate(np.eye(4), 1, icp.RULES_CLI, 3.0)  # second pass: previous-residual guesses
                 return ctx.get_correspondences()
 
-        idx, d = _with_env({"ICP_SCAN32": "1"}, run)
+        idx, d = run()
         oidx, od = oracle.OracleTree(t).nn(q, init_best=1e20)
         np.testing.assert_array_equal(idx, oidx)
         np.testing.assert_array_equal(d, od)
