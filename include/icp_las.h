@@ -38,7 +38,13 @@ int icp_las_read_header(const char* path, int rules, icp_las_header* hdr);
  * Returns the number of points read (>= 0) or a negative error as above. */
 int64_t icp_las_read(const char* path, int rules, int64_t max_points, double* xyz_out, icp_las_header* hdr);
 
+/* LASIO::writeLAS with the bounds of the given points (PointCloud::computeBounds first). */
 int icp_las_write_core(const char* path, const double* xyz, int64_t n);
+/* LASIO::writeLAS with the caller's PointCloud bounds as they stand (minX, maxX, minY, maxY, minZ,
+ * maxZ): the writer's offset is minX/minY/minZ whatever the points are now. The reference service
+ * saves the registered source with the bounds computed when it was loaded
+ * (registrationservice.cpp:98, :156), so its coordinates can fall below the offset. */
+int icp_las_write_core_bounds(const char* path, const double* xyz, int64_t n, const double bounds[6]);
 int icp_las_write_cli(const char* path, const double* xyz, int64_t n, const double scale[3], const double offset[3]);
 
 /* R row-major 3x3, t[3]; transforms: n_transforms cumulative 4x4 (row-major) or null. */

@@ -189,6 +189,7 @@ SIGNATURES = {
     "icp_las_read_header": (C.c_int, [C.c_char_p, C.c_int, C.POINTER(LasHeader)]),
     "icp_las_read": (C.c_int64, [C.c_char_p, C.c_int, C.c_int64, _P, C.POINTER(LasHeader)]),
     "icp_las_write_core": (C.c_int, [C.c_char_p, _P, C.c_int64]),
+    "icp_las_write_core_bounds": (C.c_int, [C.c_char_p, _P, C.c_int64, _P]),
     "icp_las_write_cli": (C.c_int, [C.c_char_p, _P, C.c_int64, _P, _P]),
     "icp_write_transform_report": (C.c_int, [C.c_char_p, _P, _P, _P, C.c_int32]),
 }
@@ -475,15 +476,19 @@ class Session:
 
 
 def engine_register(params: Params, src, tgt, device: int = -1, history_cap: int = 1024, stop_flag=None,
-                    on_log=None):
-    """ICPEngine::registerPointClouds drop-in. Returns (rc, result, history, src_out)."""
+                    on_log=None, on_progress=None, stop_at: int = -1):
+    """ICPEngine::registerPointClouds drop-in. Returns (rc, result, history, src_out).
+    stop_at >= 0 raises the stop flag from the progress hook of that iteration (the reference's
+    cross-thread ICPEngine::stop(), checked at the next iteration, icpengine.cpp:160)."""
     src = _aos(src).copy()
     tgt = _aos(tgt)
     res = Result()
     hist = (IterationRecord * max(1, history_cap))()
     hooks = None
     keep = []
-    if stop_flag is not None or on_log is not None:
+    if stop_at >= 0 and stop_flag is None:
+        stop_flag = C.c_int32(0)
+    if stop_flag is not None or on_log is not None or on_progress is not None:
         hooks = Hooks()
         if stop_flag is not None:
             hooks.stop_flag = C.cast(C.addressof(stop_flag), C.POINTER(C.c_int32))
@@ -491,6 +496,15 @@ def engine_register(params: Params, src, tgt, device: int = -1, history_cap: int
             cb = LOG_CB(lambda u, m: on_log(m.decode(errors="replace")))
             keep.append(cb)
             hooks.on_log = cb
+        if on_progress is not None or stop_at >= 0:
+            def _progress(_u, it, total, rmse):
+                if on_progress is not None:
+                    on_progress(it, total, rmse)
+                if stop_at >= 0 and it == stop_at:
+                    stop_flag.value = 1
+            pcb = PROGRESS_CB(_progress)
+            keep.append(pcb)
+            hooks.on_progress = pcb
     rc = lib().icp_engine_register(C.byref(params), _ptr(src), src.shape[0], _ptr(tgt), tgt.shape[0], device,
                                    C.byref(res), hist, history_cap, C.byref(hooks) if hooks else None)
     return rc, res, [hist[k] for k in range(res.n_history)], src
@@ -634,9 +648,15 @@ def las_read(path, rules=LAS_CLI, max_points=0):
     return xyz[:got], hdr
 
 
-def las_write_core(path, xyz):
+def las_write_core(path, xyz, bounds=None):
+    """LASIO::writeLAS. bounds = the caller's PointCloud (minX, maxX, minY, maxY, minZ, maxZ) as they
+    stand; None = computeBounds() of xyz."""
     xyz = _aos(xyz)
-    rc = lib().icp_las_write_core(str(path).encode(), _ptr(xyz), xyz.shape[0])
+    if bounds is None:
+        rc = lib().icp_las_write_core(str(path).encode(), _ptr(xyz), xyz.shape[0])
+    else:
+        b = np.ascontiguousarray(bounds, np.float64)
+        rc = lib().icp_las_write_core_bounds(str(path).encode(), _ptr(xyz), xyz.shape[0], _ptr(b))
     if rc != 0:
         raise IcpError(rc, f"cannot write {path}")
 

@@ -90,20 +90,10 @@ int64_t icp_las_read(const char* path, int rules, int64_t max_points, double* xy
   return got;
 }
 
-int icp_las_write_core(const char* path, const double* xyz, int64_t n) {
+int icp_las_write_core_bounds(const char* path, const double* xyz, int64_t n, const double bounds[6]) {
   if (n <= 0) return -2;  // lasio.cpp:129-132
-  // PointCloud::computeBounds (pointcloud.cpp:24-45): std::min / std::max
-  double mn[3], mx[3];
-  for (int a = 0; a < 3; a++) {
-    mn[a] = std::numeric_limits<double>::max();
-    mx[a] = std::numeric_limits<double>::lowest();
-  }
-  for (int64_t i = 0; i < n; i++)
-    for (int a = 0; a < 3; a++) {
-      const double v = xyz[3 * i + a];
-      mn[a] = (v < mn[a]) ? v : mn[a];
-      mx[a] = (mx[a] < v) ? v : mx[a];
-    }
+  if (!bounds) return -1;
+  const double mn[3] = {bounds[0], bounds[2], bounds[4]}, mx[3] = {bounds[1], bounds[3], bounds[5]};
   std::ofstream f(path, std::ios::binary);
   if (!f.is_open()) return -1;
   char h[227];
@@ -129,6 +119,23 @@ int icp_las_write_core(const char* path, const double* xyz, int64_t n) {
       wr<int32_t>(rec.data() + 20 * i + 4 * a, (int32_t)((xyz[3 * i + a] - mn[a]) / 0.001));
   f.write(rec.data(), (std::streamsize)rec.size());
   return f ? 0 : -1;
+}
+
+int icp_las_write_core(const char* path, const double* xyz, int64_t n) {
+  if (n <= 0) return -2;  // lasio.cpp:129-132
+  // PointCloud::computeBounds (pointcloud.cpp:24-45): std::min / std::max
+  double b[6];
+  for (int a = 0; a < 3; a++) {
+    b[2 * a] = std::numeric_limits<double>::max();
+    b[2 * a + 1] = std::numeric_limits<double>::lowest();
+  }
+  for (int64_t i = 0; i < n; i++)
+    for (int a = 0; a < 3; a++) {
+      const double v = xyz[3 * i + a];
+      b[2 * a] = (v < b[2 * a]) ? v : b[2 * a];
+      b[2 * a + 1] = (b[2 * a + 1] < v) ? v : b[2 * a + 1];
+    }
+  return icp_las_write_core_bounds(path, xyz, n, b);
 }
 
 int icp_las_write_cli(const char* path, const double* xyz, int64_t n, const double scale[3], const double offset[3]) {

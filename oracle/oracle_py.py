@@ -19,6 +19,9 @@ ORACLE_DIR = Path(__file__).resolve().parent
 ORACLE_LIB = ORACLE_DIR / "libicp_oracle.so"
 REF_LIB = ORACLE_DIR / "_ref" / "libicp_ref.so"
 REF_BENCH = ORACLE_DIR / "_ref" / "ref_bench"
+REF_ENGINE_LIB = ORACLE_DIR / "_ref" / "libicp_ref_engine.so"
+REF_CORE_SRC = Path("/root/reference/PointCloudRegistration/core/icpengine.cpp")
+QT_MOC = Path("/opt/conda/bin/moc")
 REFERENCE_SRC = Path("/root/reference/icp_registration.cpp")
 
 SEM_ENGINE = 0
@@ -50,6 +53,8 @@ def build(ref: bool = True) -> None:
     subprocess.run(["make", "-C", str(ORACLE_DIR), "all"], check=True, capture_output=True)
     if ref and REFERENCE_SRC.exists():
         subprocess.run(["make", "-C", str(ORACLE_DIR), "ref"], check=True, capture_output=True)
+    if ref and REF_CORE_SRC.exists() and QT_MOC.exists():
+        subprocess.run(["make", "-C", str(ORACLE_DIR), "refqt"], check=True, capture_output=True)
 
 
 _O = None
@@ -272,3 +277,67 @@ def ref_save_transformation(path, R, t, transforms):
     t = np.ascontiguousarray(t, np.float64).reshape(3)
     T = np.ascontiguousarray(transforms, np.float64).reshape(-1, 16)
     L.ref_save_transformation(str(path).encode(), _p(R), _p(t), _p(T), T.shape[0])
+
+
+# ---- the reference's core engine + LAS I/O (Qt build, fixture generation in this container only)
+
+REC_DOUBLES = 22  # iteration, rmse, valid, outliers, T_cum (16, row-major), rotation, translation
+_E = None
+
+
+def ref_engine_available() -> bool:
+    return REF_ENGINE_LIB.exists()
+
+
+def ref_engine() -> C.CDLL:
+    global _E
+    if _E is None:
+        if not REF_ENGINE_LIB.exists():
+            raise FileNotFoundError(f"{REF_ENGINE_LIB} not built (needs /root/reference and conda Qt; "
+                                    "`make -C oracle refqt`)")
+        L = C.CDLL(str(REF_ENGINE_LIB))
+        L.refeng_register.restype = C.c_int
+        L.refeng_register.argtypes = [_P, C.c_int64, _P, C.c_int64, C.c_int, C.c_double, C.c_double, C.c_int,
+                                      C.c_int, C.c_int, _P, _P, _P, _P, _P, _P, C.c_int32, _P, _P, C.c_int32]
+        L.refeng_read_las.restype = C.c_int64
+        L.refeng_read_las.argtypes = [C.c_char_p, C.c_int64, _P, C.c_int64]
+        L.refeng_write_las.restype = C.c_int
+        L.refeng_write_las.argtypes = [C.c_char_p, _P, C.c_int64, _P]
+        _E = L
+    return _E
+
+
+def ref_engine_register(src, tgt, max_iterations=50, tolerance=1e-6, sigma=3.0, max_points=10, max_depth=20,
+                        stop_at=-1):
+    """ICPEngine::setParameters + registerPointClouds of the real core/icpengine.cpp. Returns a dict:
+    finished (1 ok / 0 failed / -1 no signal), message, total_iterations, final_rmse, final_R,
+    final_t, history (k x 22), source_out."""
+    src = _aos(src)
+    tgt = _aos(tgt)
+    out = np.empty_like(src)
+    ti, fr, nh = C.c_int32(), C.c_double(), C.c_int32()
+    R, t = np.empty(9), np.empty(3)
+    cap = max(1, max_iterations + 1)
+    hist = np.zeros((cap, REC_DOUBLES))
+    msg = C.create_string_buffer(256)
+    rc = ref_engine().refeng_register(_p(src), src.shape[0], _p(tgt), tgt.shape[0], max_iterations, tolerance, sigma,
+                                      max_points, max_depth, stop_at, _p(out), C.byref(ti), C.byref(fr), _p(R),
+                                      _p(t), _p(hist), cap, C.byref(nh), msg, 256)
+    return {"finished": rc, "message": msg.value.decode("utf-8", errors="replace"),
+            "total_iterations": ti.value, "final_rmse": fr.value, "final_R": R.reshape(3, 3), "final_t": t,
+            "history": hist[: nh.value].copy(), "source_out": out}
+
+
+def ref_core_read_las(path, max_points=0, cap=20_000_000):
+    xyz = np.empty((cap, 3))
+    n = ref_engine().refeng_read_las(str(path).encode(), max_points, _p(xyz), cap)
+    return None if n < 0 else xyz[:n].copy()
+
+
+def ref_core_write_las(path, xyz, bounds=None):
+    """LASIO::writeLAS; bounds = (minX, maxX, minY, maxY, minZ, maxZ) as the caller's PointCloud
+    holds them (None: computeBounds())."""
+    xyz = _aos(xyz)
+    b = None if bounds is None else np.ascontiguousarray(bounds, np.float64)
+    return bool(ref_engine().refeng_write_las(str(path).encode(), _p(xyz), xyz.shape[0],
+                                              None if b is None else _p(b)))

@@ -119,9 +119,23 @@ int64_t refeng_read_las(const char* path, int64_t max_points, double* xyz, int64
   return n;
 }
 
-// LASIO::writeLAS (lasio.cpp:127-210). Returns 1 on success.
-int refeng_write_las(const char* path, const double* xyz, int64_t n) {
+// LASIO::writeLAS (lasio.cpp:127-210). The writer takes its offset and bounds from the cloud's
+// minX..maxZ fields: bounds (minX, maxX, minY, maxY, minZ, maxZ) sets them as a caller left them
+// (RegistrationService::saveRegisteredCloud writes the registered source with the bounds
+// computed at load time, registrationservice.cpp:98, :156); null = PointCloud::computeBounds().
+// Returns 1 on success.
+int refeng_write_las(const char* path, const double* xyz, int64_t n, const double* bounds) {
   PointCloud c = make_cloud(xyz, n);
+  if (bounds) {
+    c.minX = bounds[0];
+    c.maxX = bounds[1];
+    c.minY = bounds[2];
+    c.maxY = bounds[3];
+    c.minZ = bounds[4];
+    c.maxZ = bounds[5];
+  } else {
+    c.computeBounds();
+  }
   return LASIO::writeLAS(path, c) ? 1 : 0;
 }
 

@@ -30,6 +30,17 @@ def golden_icp():
 
 
 @pytest.fixture(scope="session")
+def golden_engine():
+    """Engine-rule cases run by the real core engine (gen_golden.py engine_cases)."""
+    return np.load(GOLDEN / "engine_rules.npz")
+
+
+@pytest.fixture(scope="session")
+def golden_core_las():
+    return np.load(GOLDEN / "core_las.npz")
+
+
+@pytest.fixture(scope="session")
 def golden_meta():
     import json
     return json.loads((GOLDEN / "golden.json").read_text())
@@ -70,3 +81,17 @@ def fnv1a(a: np.ndarray) -> str:
 
 
 KAT_CASES = ["gauss", "lattice", "duplicates", "far", "single", "root_leaf"]
+ENGINE_CASES = ["e1k", "e10k", "far", "relaxed", "params", "diverge", "too_few", "cancel"]
+
+
+def t_rmse(a, b):
+    """sqrt(mean((A - B)^2)) over the 16 entries: the north star's transform metric."""
+    return float(np.sqrt(np.mean((np.asarray(a) - np.asarray(b)) ** 2)))
+
+
+def engine_expected(golden_engine, golden_meta, name):
+    """One engine-rule case as the reference engine ran it: inputs, params and its outputs."""
+    m = golden_meta["engine_rules"][name]
+    g = {k[len(name) + 1:]: golden_engine[k] for k in golden_engine.files if k.startswith(name + "_")}
+    hist = g["history"].reshape(-1, 22)
+    return m, g, hist

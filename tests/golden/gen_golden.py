@@ -4,11 +4,13 @@
 The reference (B1AnKAlpha/IterativeClosestPoint) ships no tests, fixtures or golden data
 (SURVEY.md §4), so every vector here is produced in this container by the compiled
 reference: oracle/_ref/libicp_ref.so = /root/reference/icp_registration.cpp + its vendored
-Eigen 3.3.4, built by oracle/Makefile (`make -C oracle ref`). Inputs come from the product's
+Eigen 3.3.4, built by oracle/Makefile (`make -C oracle ref`), and oracle/_ref/libicp_ref_engine.so
+= the core engine and LAS I/O (PointCloudRegistration/core, moc + the image's conda Qt 5.9.7,
+`make -C oracle refqt`). Inputs come from the product's
 deterministic generator (icp_synth_pair) or from numpy with fixed seeds, and are stored
 alongside (or as hashes, for the 100k case).
 
-Run from the repo root:  python tests/golden/gen_golden.py
+Run from the repo root:  python tests/golden/gen_golden.py [--only-engine | --only-las]
 """
 from __future__ import annotations
 
@@ -228,9 +230,143 @@ def las_and_report():
     return {"n": n, "file_bytes": len(blob), "file_fnv1a": fnv1a(arrays["las_file"]), "trunc_cut": cut}
 
 
+def _divergent_pair():
+    """Unstructured clouds on which the reference engine stops on 'rmse > 1.1 prev'
+    (icpengine.cpp:311-314): the first such draw of a fixed-seed search."""
+    rng = np.random.default_rng(1)
+    for _ in range(2000):
+        n = int(rng.integers(50, 400))
+        tgt = rng.uniform(-1, 1, size=(n, 3)) * rng.uniform(0.2, 5, 3)
+        m = int(rng.integers(20, 400))
+        src = rng.uniform(-1, 1, size=(m, 3)) * rng.uniform(0.2, 5, 3) + rng.normal(size=3)
+        sig = float(rng.choice([0.5, 1.0, 2.0, 3.0]))
+        r = O.ref_engine_register(src, tgt, 50, 1e-6, sig)
+        if r["finished"] == 1 and r["total_iterations"] < 50 and not np.isnan(r["history"][-1][20]):
+            # ended early without the convergence record: the divergence break
+            return src, tgt, sig
+    raise RuntimeError("no divergent pair found")
+
+
+def engine_cases():
+    """The engine rules, run by the REAL core engine (core/icpengine.cpp + octree.cpp, moc, conda
+    Qt 5.9.7: oracle/_ref/libicp_ref_engine.so). Each case pins rules the CLI fixtures cannot:
+      e1k       test_icp-style 1k pair, default ICPParameters (icpengine.h:13-19)
+      e10k      10k pair to convergence: the extra convergence record with T_cumulative
+                (icpengine.cpp:293-303), final R/t = T_cumulative (:378-383)
+      far       far source points (> 1e10): DBL_MAX initial best (octree.cpp:180)
+      relaxed   near-constant residuals: the relaxed iteration-0 threshold mean + max(k std,
+                0.5 mean) (icpengine.cpp:249-252) keeps every pair
+      params    octreeMaxPoints 5, octreeMaxDepth 10, sigmaMultiplier 2
+      diverge   'error increased' break (icpengine.cpp:311-314): success with write-back
+      too_few   2 source points: finished(false) without write-back (icpengine.cpp:319-323)
+      cancel    ICPEngine::stop() during iteration 3: finished(false) at the next check
+                (icpengine.cpp:160-164), no write-back"""
+    rng = np.random.default_rng(4242)
+    cases = {}
+    angle = rng.uniform() * 10.0
+    cases["e1k"] = dict(synth=dict(n=1000, yaw_deg=angle, pitch_deg=(rng.uniform() - 0.5) * angle,
+                                   roll_deg=(rng.uniform() - 0.5) * angle,
+                                   t=[(rng.uniform() - 0.5) * 5, (rng.uniform() - 0.5) * 5, (rng.uniform() - 0.5) * 2]),
+                        params=dict(max_iterations=50, tolerance=1e-6, sigma=3.0, max_points=10, max_depth=20))
+    cases["e10k"] = dict(synth=dict(n=10000, yaw_deg=4.0, pitch_deg=1.5, roll_deg=-1.0, t=[0.4, -0.25, 0.08]),
+                         params=dict(max_iterations=80, tolerance=1e-9, sigma=3.0, max_points=10, max_depth=20))
+    t = rng.normal(size=(3000, 3)) * [4, 4, 1]
+    s = np.concatenate([t[:1500] + rng.normal(size=(1500, 3)) * 0.01 + [0.05, -0.02, 0.01],
+                        rng.normal(size=(4, 3)) * 3e10])
+    cases["far"] = dict(src=s, tgt=t, params=dict(max_iterations=10, tolerance=1e-6, sigma=3.0, max_points=10,
+                                                  max_depth=20))
+    t = rng.uniform(-2, 2, size=(4000, 3))
+    s = t[rng.permutation(4000)[:2000]] + [0.01, -0.004, 0.002] + rng.normal(size=(2000, 3)) * 1e-5
+    cases["relaxed"] = dict(src=s, tgt=t, params=dict(max_iterations=6, tolerance=1e-6, sigma=3.0, max_points=10,
+                                                      max_depth=20))
+    cases["params"] = dict(synth=dict(n=6000, yaw_deg=-3.0, pitch_deg=0.5, roll_deg=2.0, t=[-0.2, 0.3, 0.1]),
+                           params=dict(max_iterations=25, tolerance=1e-7, sigma=2.0, max_points=5, max_depth=10))
+    s, t, sig = _divergent_pair()
+    cases["diverge"] = dict(src=s, tgt=t, params=dict(max_iterations=50, tolerance=1e-6, sigma=sig, max_points=10,
+                                                      max_depth=20))
+    t = rng.normal(size=(100, 3))
+    cases["too_few"] = dict(src=t[:2] + 0.01, tgt=t, params=dict(max_iterations=50, tolerance=1e-6, sigma=3.0,
+                                                                 max_points=10, max_depth=20))
+    cases["cancel"] = dict(synth=dict(n=3000, yaw_deg=5.0, pitch_deg=0.0, roll_deg=0.0, t=[0.3, 0.1, 0.0]),
+                           params=dict(max_iterations=50, tolerance=1e-9, sigma=3.0, max_points=10, max_depth=20),
+                           stop_at=3)
+    arrays, meta = {}, {}
+    for name, c in cases.items():
+        if "synth" in c:
+            sp = c["synth"]
+            tgt, src, _ = icp.synth_pair(sp["n"], yaw_deg=sp["yaw_deg"], pitch_deg=sp["pitch_deg"],
+                                         roll_deg=sp["roll_deg"], t=sp["t"])
+        else:
+            src, tgt = np.ascontiguousarray(c["src"]), np.ascontiguousarray(c["tgt"])
+        p = c["params"]
+        r = O.ref_engine_register(src, tgt, p["max_iterations"], p["tolerance"], p["sigma"], p["max_points"],
+                                  p["max_depth"], c.get("stop_at", -1))
+        arrays[f"{name}_source"] = src
+        arrays[f"{name}_target"] = tgt
+        arrays[f"{name}_history"] = r["history"]
+        arrays[f"{name}_source_out"] = r["source_out"]
+        arrays[f"{name}_final_R"] = r["final_R"]
+        arrays[f"{name}_final_t"] = r["final_t"]
+        meta[name] = {"params": p, "stop_at": c.get("stop_at", -1), "finished": r["finished"],
+                      "message": r["message"], "total_iterations": r["total_iterations"],
+                      "final_rmse": r["final_rmse"], "n_history": int(len(r["history"]))}
+    np.savez_compressed(OUT / "engine_rules.npz", **arrays)
+    return meta
+
+
+def core_las():
+    """The core LASIO (core/lasio.cpp, Qt build): writeLAS bytes, readLAS with and without the
+    maxPoints truncation (lasio.cpp:60-63), readLAS of the CLI writer's file."""
+    import tempfile
+    rng = np.random.default_rng(78)
+    n = 10007
+    xyz = np.stack([rng.normal(0, 30, n) + 4.0e5, rng.normal(0, 20, n) + 3.2e6, rng.normal(0, 3, n) + 12.0], 1)
+    xyz[:3] = [[4.0e5, 3.2e6, 12.0], [4.0e5 - 0.0004999, 3.2e6 + 0.0005001, 11.9995], [4.1e5, 3.1e6, -7.0]]
+    arrays = {"core_points": xyz}
+    G = np.load(OUT / "las_report.npz")
+    with tempfile.TemporaryDirectory() as d:
+        f = Path(d) / "core.las"
+        assert O.ref_core_write_las(f, xyz)
+        blob = f.read_bytes()
+        arrays["core_file"] = np.frombuffer(blob, np.uint8)
+        arrays["core_read"] = O.ref_core_read_las(f)
+        arrays["core_read_max"] = O.ref_core_read_las(f, max_points=1234)
+        # the registered source written with the bounds of the cloud as loaded (stale: the
+        # service never recomputes them after registration, registrationservice.cpp:98, :156)
+        moved = xyz + [0.7, -1.3, 0.25]
+        stale = np.array([xyz[:, 0].min(), xyz[:, 0].max(), xyz[:, 1].min(), xyz[:, 1].max(),
+                          xyz[:, 2].min(), xyz[:, 2].max()])
+        h = Path(d) / "stale.las"
+        assert O.ref_core_write_las(h, moved, stale)
+        arrays["core_moved"] = moved
+        arrays["core_stale_bounds"] = stale
+        arrays["core_file_stale"] = np.frombuffer(h.read_bytes(), np.uint8)
+        g = Path(d) / "cli.las"
+        g.write_bytes(G["las_file"].tobytes())
+        arrays["core_read_cli_file"] = O.ref_core_read_las(g)
+        arrays["core_read_cli_file_max"] = O.ref_core_read_las(g, max_points=10001)
+        z = bytearray(G["las_file"].tobytes()[:227])
+        z[107:111] = (0).to_bytes(4, "little")
+        (Path(d) / "z.las").write_bytes(bytes(z))
+        rz = O.ref_core_read_las(Path(d) / "z.las")
+        arrays["core_zero_points"] = np.array([-1 if rz is None else len(rz)])
+    np.savez_compressed(OUT / "core_las.npz", **arrays)
+    return {"n": n, "file_bytes": len(blob), "file_fnv1a": fnv1a(arrays["core_file"])}
+
+
 def main():
     if not O.reference_available():
         O.build(ref=True)
+    if "--only-engine" in sys.argv:
+        meta = json.loads((OUT / "golden.json").read_text())
+        meta["engine_rules"] = engine_cases()
+        meta["core_las"] = core_las()
+        meta["engine_reference"] = ("PointCloudRegistration/core/{icpengine,octree,pointcloud,lasio}.cpp + moc, "
+                                    "Qt 5.9.7 (/opt/conda), g++ -O2 -ffp-contract=off, no -march "
+                                    "(oracle/_ref/libicp_ref_engine.so)")
+        (OUT / "golden.json").write_text(json.dumps(meta, indent=1, sort_keys=True))
+        print(json.dumps({k: meta[k] for k in ("engine_rules", "core_las")}, indent=1))
+        return
     if "--only-las" in sys.argv:
         meta = json.loads((OUT / "golden.json").read_text())
         meta["las_report"] = las_and_report()
@@ -244,6 +380,11 @@ def main():
     meta["icp_cli"] = icp_cli_cases()
     meta["nn_100k"] = nn_100k_hashes()
     meta["las_report"] = las_and_report()
+    meta["engine_rules"] = engine_cases()
+    meta["core_las"] = core_las()
+    meta["engine_reference"] = ("PointCloudRegistration/core/{icpengine,octree,pointcloud,lasio}.cpp + moc, "
+                                "Qt 5.9.7 (/opt/conda), g++ -O2 -ffp-contract=off, no -march "
+                                "(oracle/_ref/libicp_ref_engine.so)")
     (OUT / "golden.json").write_text(json.dumps(meta, indent=1, sort_keys=True))
     print(json.dumps(meta, indent=1))
 

@@ -9,7 +9,7 @@ final 4x4 transform within 1e-6 RMSE of the CPU/Eigen reference (observed ~1e-14
 import numpy as np
 import pytest
 
-from conftest import KAT_CASES, fnv1a
+from conftest import ENGINE_CASES, KAT_CASES, engine_expected, fnv1a
 
 pytestmark = pytest.mark.gpu
 
@@ -147,6 +147,45 @@ def test_engine_register_vs_oracle(icp, oracle, n, yaw):
     np.testing.assert_allclose(out, oout, atol=1e-9)
     for h, o in zip(hist, ohist):
         np.testing.assert_allclose(np.array(h.transform), np.array(o.T_cum), atol=1e-10)
+
+
+@pytest.mark.parametrize("name", ENGINE_CASES)
+def test_engine_register_vs_core_reference(icp, golden_engine, golden_meta, name):
+    """The product's ICPEngine drop-in (icp_engine_register: device search + statistics, host SVD)
+    against the REAL core engine (core/icpengine.cpp + moc + conda Qt, tests/golden/engine_rules.npz):
+    iteration count, per-iteration valid/outlier counts and RMSE, cumulative transforms, the
+    convergence record, final R/t = T_cumulative within 1e-6 RMSE (observed ~1e-15), write-back
+    or none, the divergence break, cancellation via stop() at iteration 3."""
+    m, g, hist = engine_expected(golden_engine, golden_meta, name)
+    p = m["params"]
+    params = icp.params_default(max_iterations=p["max_iterations"], tolerance=p["tolerance"],
+                                sigma_multiplier=p["sigma"], octree_max_points=p["max_points"],
+                                octree_max_depth=p["max_depth"])
+    rc, res, rh, out = icp.engine_register(params, g["source"], g["target"], device=0, stop_at=m["stop_at"])
+    assert len(rh) == len(hist)
+    for r, h in zip(rh, hist):
+        assert r.iteration == int(h[0]) and r.valid_points == int(h[2]) and r.outlier_points == int(h[3])
+        np.testing.assert_allclose(r.rmse, h[1], rtol=1e-9, atol=1e-15)
+        np.testing.assert_allclose(np.array(r.transform).reshape(4, 4), h[4:20].reshape(4, 4), atol=1e-10)
+        if r.has_transform:
+            np.testing.assert_allclose([r.rotation_angle_deg, r.translation_distance], h[20:22], rtol=1e-6, atol=1e-9)
+        else:  # the convergence record leaves them unset in the reference
+            assert np.isnan(h[20])
+    if m["finished"] == 0:
+        assert rc != 0 and not res.success
+        np.testing.assert_array_equal(out, g["source"])  # finished(false): no write-back
+        return
+    assert rc == 0 and res.success and res.total_iterations == m["total_iterations"]
+    T = np.eye(4)
+    T[:3, :3] = np.array(res.final_R).reshape(3, 3)
+    T[:3, 3] = res.final_t
+    Tr = np.eye(4)
+    Tr[:3, :3] = g["final_R"]
+    Tr[:3, 3] = g["final_t"]
+    assert t_rmse(T, Tr) < RMSE_TOL
+    np.testing.assert_allclose(T, Tr, atol=1e-10)
+    np.testing.assert_allclose(res.final_rmse, m["final_rmse"], rtol=1e-9, atol=1e-15)
+    np.testing.assert_allclose(out, g["source_out"], atol=1e-9)
 
 
 def test_engine_too_few_pairs_keeps_source(icp):

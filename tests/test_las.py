@@ -1,10 +1,11 @@
 """LAS 1.2 I/O and the transformation report against the reference's own output.
 
-Fixtures: tests/golden/las_report.npz, written by the compiled reference (saveResultAsLAS,
-readLASFile, saveTransformation — icp_registration.cpp:248-378, :625-815) via
-tests/golden/gen_golden.py. The core LASIO (core/lasio.cpp) needs Qt headers and cannot be built
-here: its reader shares readLASFile's arithmetic (pinned below); its writer is a restatement whose
-round-trip properties are checked, parity unpinned.
+Fixtures, written by the compiled reference via tests/golden/gen_golden.py:
+  las_report.npz  the CLI's saveResultAsLAS / readLASFile / saveTransformation
+                  (icp_registration.cpp:248-378, :625-815)
+  core_las.npz    the core LASIO::writeLAS / readLAS (core/lasio.cpp:7-210), built with moc and
+                  the image's conda Qt (oracle/_ref/libicp_ref_engine.so): bytes of the writer,
+                  the reader with and without maxPoints truncation.
 """
 from __future__ import annotations
 
@@ -79,9 +80,46 @@ def test_missing_file(tmp_path):
         _lib.las_read(tmp_path / "nope.las")
 
 
+CORE = np.load(Path(__file__).parent / "golden" / "core_las.npz")
+
+
+def test_core_writer_byte_identical(tmp_path):
+    """LASIO::writeLAS (core/lasio.cpp:127-210) on a computeBounds()'d cloud: the same bytes."""
+    f = tmp_path / "c.las"
+    _lib.las_write_core(f, CORE["core_points"])
+    assert f.read_bytes() == CORE["core_file"].tobytes()
+
+
+def test_core_writer_stale_bounds_byte_identical(tmp_path):
+    """RegistrationService::saveRegisteredCloud writes the registered source with the bounds of
+    the cloud as loaded (registrationservice.cpp:98, :156): offset = the old minimum, and the
+    truncating cast of coordinates now below it. Same bytes as the reference."""
+    f = tmp_path / "s.las"
+    _lib.las_write_core(f, CORE["core_moved"], bounds=CORE["core_stale_bounds"])
+    assert f.read_bytes() == CORE["core_file_stale"].tobytes()
+
+
+def test_core_reader_matches_reference(tmp_path):
+    """LASIO::readLAS, all points and maxPoints truncation (lasio.cpp:60-63), on the core writer's
+    file and on the CLI writer's (two batches of 10000 with a ragged tail)."""
+    f = tmp_path / "c.las"
+    f.write_bytes(CORE["core_file"].tobytes())
+    xyz, _ = _lib.las_read(f, _lib.LAS_CORE)
+    assert xyz.tobytes() == CORE["core_read"].tobytes()
+    xyz, _ = _lib.las_read(f, _lib.LAS_CORE, max_points=1234)
+    assert xyz.tobytes() == CORE["core_read_max"].tobytes()
+    g = tmp_path / "cli.las"
+    g.write_bytes(G["las_file"].tobytes())
+    xyz, _ = _lib.las_read(g, _lib.LAS_CORE)
+    assert xyz.tobytes() == CORE["core_read_cli_file"].tobytes()
+    xyz, _ = _lib.las_read(g, _lib.LAS_CORE, max_points=10001)
+    assert xyz.tobytes() == CORE["core_read_cli_file_max"].tobytes()
+    assert int(CORE["core_zero_points"][0]) == 0  # readLAS accepts a zero-point file (empty cloud)
+
+
 def test_core_writer_roundtrip(tmp_path):
-    """LASIO::writeLAS restatement (core/lasio.cpp:127-210): scale 0.001, offset = bounds min,
-    truncating casts. Parity unpinned (Qt); checked through its defining properties."""
+    """LASIO::writeLAS properties (core/lasio.cpp:127-210): scale 0.001, offset = bounds min,
+    truncating casts; reading back is within one quantum."""
     pts = G["las_points"][:5000]
     f = tmp_path / "c.las"
     _lib.las_write_core(f, pts)
