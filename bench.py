@@ -2,7 +2,7 @@
 """bench.py — Mcorr/s per ICP iteration on MI355X (BASELINE.json metric), config 4 by default:
 10M <-> 10M synthetic clouds, source sharded over the ranks, target octree replicated.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--n 10000000]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--points 10000000]
     torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU)
 
 A step = one full ICP iteration of the product engine (icp_session_step): fused transform of
@@ -10,16 +10,28 @@ the resident source + exact octree NN + residual + 3-sigma statistics (RCCL all-
 + centroid/covariance (RCCL all-gather) + host 3x3 SVD. Convergence stops are disabled
 (ICP_FLAG_NO_EARLY_STOP) so exactly K iterations are timed.
 
-Rank 0 prints ONE JSON line. Extra objects:
-  roofline      the search kernel's algorithmic bytes per launch (SURVEY.md §8d byte model:
-                148 + 56 V + 24 P bytes per correspondence, V/P = node entries / leaf points of the
-                reference DFS, counted exactly by the kernel) / its average HIP-event duration.
+Rank 0 prints ONE JSON line. `value` = the points of all ranks x K / the wall time of the K timed
+iterations (max over ranks); `median` = the same rate from the median iteration of 2..K
+(SURVEY.md §8d). Extra objects:
+  roofline      the search kernel k_nn_wave: its compulsory HBM bytes per launch (DESIGN.md §5:
+                68 B per query streamed + every target point (28 B) and node (56 B) once) / its
+                average HIP-event duration over the timed iterations; `traffic` = PMC bytes per
+                launch (rocprofv3, calibrated per access width: tools/calib_pmc.sh) of the same
+                kernel source, or null.
+  reference_work  SURVEY.md §8d's model of the reference DFS's work (148 + 56 V + 24 P bytes per
+                correspondence): what the reference would move, not what this kernel moves.
   cpu_baseline  the REFERENCE CPU path (oracle/_ref/ref_bench: icp_registration.cpp's ICP()),
                 1 thread, on a bounded sample of the same workload (rank 0, N=1 only).
+  cpu_allcores  the CPU restatement (oracle/icp_oracle.c, OpenMP NN loop) on every core of this
+                process's CPU set, full size, from the parity leg below.
+  parity        (N=1) a fresh engine registration of the full clouds for --parity-iters
+                iterations on the GPU and on the CPU oracle: final transform RMSE (north star:
+                <= 1e-6), per-iteration valid counts, final RMSE.
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
 import platform
@@ -37,7 +49,20 @@ sys.path.insert(0, str(ROOT))
 METRIC = "M correspondences/sec per ICP iter at 1/2/4/8 GPUs; final RMSE vs CPU ref"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
 # BASELINE.json configs by cloud size (config 3 is the LAS pair: tests/test_gpu_lasflow.py)
-CONFIG_NAMES = {100_000: "config2", 10_000_000: "config4", 50_000_000: "config5"}
+CONFIG_NAMES = {100_000: "config2", 1_000_000: "config3-size", 10_000_000: "config4", 50_000_000: "config5"}
+SEARCH_SOURCES = ("nn_kernels.hip", "nn_device.h", "kernels.h")
+# compulsory bytes of one k_nn_wave<true> launch
+STREAM_B_PER_QUERY = 24 + 24 + 8 + 4 + 8  # source read + transformed write, guess, pos + dist
+TGT_B_PER_POINT = 28  # x, y, z + original index of a leaf-ordered target point
+NODE_B = 56  # box (48 B) + topology (8 B) of a node record
+
+
+def search_source_sha1() -> str:
+    """Hash of the search kernel's sources: a PMC profile counts only for the code it measured."""
+    h = hashlib.sha1()
+    for f in SEARCH_SOURCES:
+        h.update((ROOT / "iterativeclosestpoint_amd" / "csrc" / f).read_bytes())
+    return h.hexdigest()
 
 
 def shard_range(n: int, rank: int, world: int) -> tuple[int, int]:
@@ -47,7 +72,14 @@ def shard_range(n: int, rank: int, world: int) -> tuple[int, int]:
     return lo, lo + base + (1 if rank < rem else 0)
 
 
-def bytes_per_corr(v: float, p: float) -> float:
+def compulsory_bytes(n_local: int, n_total: int, n_tgt: int, n_nodes: int) -> float:
+    """HBM bytes one search launch cannot avoid: its queries streamed once, and the target points
+    and nodes once (a spatial shard touches about its share of them)."""
+    share = n_local / max(1, n_total)
+    return STREAM_B_PER_QUERY * n_local + (TGT_B_PER_POINT * n_tgt + NODE_B * n_nodes) * share
+
+
+def reference_bytes_per_corr(v: float, p: float) -> float:
     # SURVEY.md §8(d): query 24 + idx 4 + residual 8 (NN pass); residual 8 (sigma pass);
     # residual 8 + query 24 + idx 4 + gather 24 (cull/covariance); transform r+w 48;
     # 56 B per node entry (48 B box + 8 B topology); 24 B per leaf point scanned.
@@ -63,6 +95,15 @@ def cpu_model() -> str:
     except Exception:
         pass
     return platform.processor() or "unknown"
+
+
+def cpu_threads() -> int:
+    """Cores of this process's CPU share: the affinity set, capped by OMP_NUM_THREADS if set."""
+    n = len(os.sched_getaffinity(0))
+    env = os.environ.get("OMP_NUM_THREADS", "")
+    if env.isdigit() and int(env) > 0:
+        n = min(n, int(env))
+    return max(1, n)
 
 
 def cpu_baseline(tgt: np.ndarray, src: np.ndarray, sample: int) -> dict | None:
@@ -85,7 +126,8 @@ def cpu_baseline(tgt: np.ndarray, src: np.ndarray, sample: int) -> dict | None:
                         "sample": f"{len(pick)} of {len(src)} source queries vs the full {len(tgt)}-point target; "
                                   f"one reference ICP() iteration (icp_registration.cpp:443-622, g++ -O2) = "
                                   f"t(ICP 2 iters) - t(ICP 1 iter) = {j['iter_s']:.2f} s; CPU {cpu_model()}"}
-    # fallback: the C restatement (oracle/icp_oracle.c), same iteration difference
+    # fallback: the C restatement (oracle/icp_oracle.c), same iteration difference, one thread
+    oracle_py.set_threads(1)
     t0 = time.perf_counter()
     oracle_py.icp(src[pick], tgt, oracle_py.SEM_CLI, 1, 1e-300)
     t1 = time.perf_counter()
@@ -96,19 +138,73 @@ def cpu_baseline(tgt: np.ndarray, src: np.ndarray, sample: int) -> dict | None:
             "sample": f"{len(pick)} of {len(src)} queries vs full target, oracle/icp_oracle.c, CPU {cpu_model()}"}
 
 
+def parity_leg(icp, ctx, tgt: np.ndarray, src: np.ndarray, iters: int) -> tuple[dict, dict]:
+    """A fresh engine registration (tolerance 0: exactly `iters` iterations) of the full clouds on
+    the GPU and on the CPU oracle (OpenMP over all cores of this process). Returns the parity
+    record and the all-core CPU throughput (per-iteration time = (ICP time - octree build) / iters)."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import oracle_py  # test infrastructure: the checker and the CPU baseline leg only
+
+    ctx.set_source(src)
+    sess = ctx.session(icp.params_default(max_iterations=iters, tolerance=0.0))
+    g_valid, g_rmse = [], []
+    while not sess.done:
+        rec = sess.step()
+        if rec is not None:
+            g_valid.append(int(rec.valid_points))
+            g_rmse.append(float(rec.rmse))
+    rc, res = sess.finish()
+    sess.close()
+    Tg = np.eye(4)
+    Tg[:3, :3] = np.array(res.final_R).reshape(3, 3)
+    Tg[:3, 3] = res.final_t
+
+    cores = cpu_threads()
+    oracle_py.set_threads(cores)
+    t0 = time.perf_counter()
+    oracle_py.OracleTree(tgt)  # the octree build inside ICP, timed alone (single-threaded)
+    t_build = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    orc, ores, ohist, _ = oracle_py.icp(src, tgt, oracle_py.SEM_ENGINE, iters, 0.0)
+    t_icp = time.perf_counter() - t0
+    To = np.eye(4)
+    To[:3, :3] = np.array(ores.final_R).reshape(3, 3)
+    To[:3, 3] = ores.final_t
+    o_valid = [int(h.valid) for h in ohist if h.has_transform]
+    o_rmse = [float(h.rmse) for h in ohist if h.has_transform]
+    rel = [abs(a - b) / max(abs(b), 1e-300) for a, b in zip(g_rmse, o_rmse)]
+    parity = {
+        "iterations": iters,
+        "final_transform_rmse_vs_cpu": float(np.sqrt(np.mean((Tg - To) ** 2))),
+        "tolerance": 1e-6,
+        "iterations_equal": res.total_iterations == ores.total_iterations,
+        "valid_counts_equal": g_valid == o_valid,
+        "final_rmse_gpu": res.final_rmse, "final_rmse_cpu": ores.final_rmse,
+        "rmse_max_rel_diff": max(rel) if rel else None,
+        "checker": "oracle/icp_oracle.c engine rules (pinned to core/icpengine.cpp by tests/golden/engine_rules.npz)",
+    }
+    per_iter = max(1e-9, (t_icp - t_build) / iters)
+    allcores = {"value": round(len(src) / per_iter / 1e6, 4), "unit": "Mcorr/s", "cores": cores, "kind": "port",
+                "sample": f"full {len(src)}<->{len(tgt)} engine ICP, {iters} iterations: ({t_icp:.1f} s - "
+                          f"{t_build:.1f} s octree build) / {iters}; OpenMP NN loop, CPU {cpu_model()}"}
+    return parity, allcores
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--points", type=int, default=10_000_000, help="points per cloud (config 4: 10M)")
     ap.add_argument("--cpu-sample", type=int, default=1_000_000)
+    ap.add_argument("--parity-iters", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--exchange", choices=("rccl", "host"), default="rccl",
                     help="per-iteration all-gathers: RCCL (default), or over torch.distributed gloo "
                          "through the host (rehearsal of N ranks on one GPU; RCCL refuses that)")
     ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "traffic_latest.json"),
-                    help="PMC-derived HBM bytes per search launch (written by tools/pmc_traffic.py)")
+                    help="PMC-derived bytes per search launch (written by tools/pmc_traffic.py)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -121,7 +217,10 @@ def main() -> int:
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("gloo", rank=rank, world_size=world)
-    device = local_rank % max(1, torch.cuda.device_count())  # ranks > GPUs only in rehearsals
+    n_dev = max(1, torch.cuda.device_count())
+    device = local_rank % n_dev  # ranks > GPUs only in host-exchange rehearsals
+    gpus_used = min(world, n_dev)
+    shared_gpu = world > gpus_used
     torch.cuda.set_device(device)
 
     n = args.points
@@ -150,65 +249,74 @@ def main() -> int:
     params = icp.params_default(max_iterations=args.warmup + args.steps + 1, tolerance=1e-6,
                                 flags=icp.FLAG_NO_EARLY_STOP)
     sess = ctx.session(params)
-    for _ in range(args.warmup):
-        sess.step()
+    # warmup; the first iteration (no previous residuals: the guess is a descent) is reported alone
+    first_ms = sess.step_n_timed(1)
+    first_nn_ms, _ = ctx.timings(1)
+    if args.warmup > 1:
+        sess.step_n_timed(args.warmup - 1)
     ctx.synchronize()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
-    taken = sess.step_n(args.steps)  # the engine's own loop, K iterations (no early stop)
+    step_ms = sess.step_n_timed(args.steps)  # the engine's own loop, K iterations (no early stop)
     ctx.synchronize()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    assert taken == args.steps, f"only {taken} of {args.steps} iterations ran"
+    assert len(step_ms) == args.steps, f"only {len(step_ms)} of {args.steps} iterations ran"
+    med_ms = float(np.median(step_ms[1:] if len(step_ms) > 1 else step_ms))
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64)
+        t = torch.tensor([elapsed, med_ms], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed, med_ms = float(t[0].item()), float(t[1].item())
     # HIP events of the timed iterates (read after the timed region)
-    nn_ms, it_ms = ctx.timings(min(args.steps, 64))
+    nn_ms, it_ms = ctx.timings(min(args.steps, 256))
     # untimed: how the last timed state splits over the search paths (same queries, same guess)
     probe = ctx.iterate(None, 1, icp.RULES_ENGINE, 3.0)
     rc, res = sess.finish()
+    sess.close()
+    # v, p of the reference DFS on this rank's queries (untimed; COUNT build of the parity kernel)
+    v_mean, p_mean = ctx.traversal_counts() if rank == 0 else (None, None)
 
-    # untimed: reference-DFS work of this rank's queries (the V, P of the byte model)
-    v_mean, p_mean = ctx.traversal_counts()
+    info = ctx.target_info()
     n_local = hi - lo
     nn_avg_s = float(np.mean(nn_ms)) / 1e3
-    b_corr = bytes_per_corr(v_mean, p_mean)
-    achieved = b_corr * n_local / nn_avg_s / 1e9
+    need = compulsory_bytes(n_local, n, n, info["n_nodes"])
+    achieved = need / nn_avg_s / 1e9
     traffic = None
     tj = Path(args.traffic_json)
     if tj.exists():
         try:
             tr = json.loads(tj.read_text())
-            import hashlib
-            kh = hashlib.sha1((ROOT / "iterativeclosestpoint_amd" / "csrc" / "kernels.hip").read_bytes()).hexdigest()
             # only a profile of this exact kernel source and workload counts
-            if tr.get("n") == n and tr.get("world") == world and tr.get("kernels_hip_sha1") == kh:
-                traffic = tr.get("hbm_bytes_per_launch")
+            if tr.get("n") == n and tr.get("world") == world and tr.get("search_src_sha1") == search_source_sha1():
+                traffic = tr.get("bytes_per_launch")
         except Exception:
             traffic = None
 
     value = n * args.steps / elapsed / 1e6
 
-    cpu = None
+    cpu = allcores = parity = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             cpu = cpu_baseline(tgt, src, args.cpu_sample)
         except Exception as e:  # keep the bench line even if the baseline cannot run
             cpu = {"value": None, "unit": "Mcorr/s", "cores": 1, "kind": "reference", "sample": f"failed: {e}"}
+    if rank == 0 and world == 1 and not args.no_parity and args.parity_iters > 0:
+        try:
+            parity, allcores = parity_leg(icp, ctx, tgt, src, args.parity_iters)
+        except Exception as e:
+            parity = {"error": str(e)}
 
     if rank == 0:
-        info = ctx.target_info()
+        nq = max(1, n_local)
         line = {
             "metric": METRIC,
             "value": round(value, 3),
             "unit": "Mcorr/s",
-            "n_gpus": world,
+            "n_gpus": gpus_used,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
@@ -221,27 +329,38 @@ def main() -> int:
             "config": {
                 "workload": f"{CONFIG_NAMES.get(n, 'custom')}: {n}<->{n} synthetic pair, full ICP iteration "
                             f"(engine rules, octree leaf 10 / depth 20), "
-                            f"source sharded over {world} GPU(s), target octree replicated",
-                "n_target": n, "n_source": n, "parallelism": f"spatial source shards x{world} (kd-order ranges; "
-                + ("RCCL" if args.exchange == "rccl" else "host/gloo") + " all-gather of 2 moment records per iteration)",
+                            f"source sharded over {world} rank(s) on {gpus_used} GPU(s), target octree replicated",
+                "n_target": n, "n_source": n, "ranks": world, "ranks_per_gpu": world // gpus_used,
+                "parallelism": f"spatial source shards x{world} (kd-order ranges; "
+                + ("RCCL" if args.exchange == "rccl" else "host/gloo rehearsal") + " all-gather of 2 moment records per iteration)",
                 "octree_nodes": info["n_nodes"], "octree_leaves": info["n_leaves"],
             },
-            "roofline": {
+            "median": {"iter_ms": round(med_ms, 4), "value": round(n / med_ms / 1e3, 3),
+                       "over": f"iterations 2..{args.steps} of the timed region (host wall per step, max over ranks)"},
+            "first_iteration": {"ms": round(float(first_ms[0]), 4), "search_kernel_ms": round(float(first_nn_ms[0]), 4),
+                                "note": "no previous residuals: the guess is a descent, the search kernel is k_nn_wave<false>"},
+            # ranks sharing one GPU (host-exchange rehearsal) contend for it: no per-rank roofline
+            "roofline": None if shared_gpu else {
                 "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                # the measured side: PMC HBM bytes per launch / the same launch time (the model above
-                # prices every node entry as an HBM read; most are L2/MALL hits, so frac can exceed 1)
-                "traffic_gbs": None if traffic is None else round(traffic / nn_avg_s / 1e9, 1),
-                "traffic_frac": None if traffic is None else round(traffic / nn_avg_s / 1e9 / HBM_PEAK_GBS, 4),
-                "kernel": "k_nn4 (fused transform + wave-cooperative certified octree NN + residual + block moments)",
-                "bytes_per_corr": round(b_corr, 1), "node_entries_per_query": round(v_mean, 3),
-                "leaf_points_per_query": round(p_mean, 3), "kernel_ms_avg": round(float(np.mean(nn_ms)), 4),
+                "traffic_over_algorithmic": None if traffic is None else round(traffic / need, 3),
+                "kernel": "k_nn_wave<true> (fused transform + wave-cooperative certified octree NN + residual)",
+                "algorithmic_bytes_per_launch": round(need), "kernel_ms_avg": round(float(np.mean(nn_ms)), 4),
                 "iterate_device_ms_avg": round(float(np.mean(it_ms)), 4),
-                "exact_fallback_queries": int(probe.n_fallback),
-                "lane_search_queries": int(probe.n_lane_search),
-                "ball_search_queries": int(probe.n_ball_search),
+                "model": f"{STREAM_B_PER_QUERY} B/query streamed + {TGT_B_PER_POINT} B/target point + {NODE_B} B/node, each once",
             },
+            "search_paths": {"queries": n_local, "wave": n_local - int(probe.n_ball_search),
+                             "ball": int(probe.n_ball_search), "lane": int(probe.n_lane_search),
+                             "exact_fallback": int(probe.n_fallback),
+                             "ball_share": round(probe.n_ball_search / nq, 6),
+                             "fallback_share": round(probe.n_fallback / nq, 6)},
+            "reference_work": None if v_mean is None else {
+                "node_entries_per_query": round(v_mean, 3), "leaf_points_per_query": round(p_mean, 3),
+                "bytes_per_corr": round(reference_bytes_per_corr(v_mean, p_mean), 1),
+                "note": "SURVEY.md §8d model of the reference DFS's work; the certified search does not do it"},
             "cpu_baseline": cpu,
+            "cpu_allcores": allcores,
+            "parity": parity,
             "setup_s": round(setup_s, 2),
             "octree_build": {"on_device": build_on_dev, "ms": round(build_ms, 2)},
             "final_rmse": res.final_rmse,

@@ -110,6 +110,9 @@ int icp_session_step(icp_session* s, icp_iteration_record* rec, int32_t* produce
 /* Up to k steps in one call (no records returned; hooks still fire); stops early when the loop
  * is done. *steps_done = steps taken. Same as calling icp_session_step k times. */
 int icp_session_step_n(icp_session* s, int32_t k, int32_t* steps_done, int32_t* done);
+/* icp_session_step_n that also stores each step's host wall time (ms, steady clock; the step
+ * returns when its record is on the host, so this is the whole iteration). step_ms[k]. */
+int icp_session_step_n_timed(icp_session* s, int32_t k, int32_t* steps_done, int32_t* done, double* step_ms);
 int icp_session_finish(icp_session* s, icp_result* res);
 /* Current cumulative transform (row-major 4x4). */
 void icp_session_transform(const icp_session* s, double T_cum[16]);

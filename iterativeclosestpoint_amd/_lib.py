@@ -162,6 +162,7 @@ SIGNATURES = {
     "icp_session_create": (C.c_int, [_P, C.POINTER(Params), C.POINTER(Hooks), C.POINTER(C.c_void_p)]),
     "icp_session_step": (C.c_int, [_P, C.POINTER(IterationRecord), _I32, _I32]),
     "icp_session_step_n": (C.c_int, [_P, C.c_int32, _I32, _I32]),
+    "icp_session_step_n_timed": (C.c_int, [_P, C.c_int32, _I32, _I32, _P]),
     "icp_session_finish": (C.c_int, [_P, C.POINTER(Result)]),
     "icp_session_transform": (None, [_P, _P]),
     "icp_session_destroy": (None, [_P]),
@@ -452,6 +453,15 @@ class Session:
         self.done = bool(done.value)
         _check(rc)
         return n.value
+
+    def step_n_timed(self, k: int) -> np.ndarray:
+        """Up to k steps in one native call; returns each step's host wall time (ms)."""
+        ms = np.zeros(max(1, k))
+        n, done = C.c_int32(0), C.c_int32(0)
+        rc = lib().icp_session_step_n_timed(self._h, k, C.byref(n), C.byref(done), _ptr(ms))
+        self.done = bool(done.value)
+        _check(rc)
+        return ms[: n.value]
 
     def transform(self) -> np.ndarray:
         T = np.empty(16)

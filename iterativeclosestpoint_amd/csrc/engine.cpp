@@ -8,6 +8,7 @@
 //   -> T is applied at the start of the next iterate (or explicitly after the loop).
 #include <cfloat>
 #include <cstdarg>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -244,6 +245,24 @@ int icp_session_step_n(icp_session* s, int32_t k, int32_t* steps_done, int32_t* 
   while (n < k && !d) {
     rc = icp_session_step(s, nullptr, nullptr, &d);
     if (rc != ICP_HIP_OK) break;
+    n++;
+  }
+  if (steps_done) *steps_done = n;
+  if (done) *done = d;
+  return rc;
+}
+
+int icp_session_step_n_timed(icp_session* s, int32_t k, int32_t* steps_done, int32_t* done, double* step_ms) {
+  if (!s || k < 0 || (k > 0 && !step_ms)) return ICP_HIP_EINVAL;
+  int32_t n = 0, d = 0;
+  int rc = ICP_HIP_OK;
+  auto t0 = std::chrono::steady_clock::now();
+  while (n < k && !d) {
+    rc = icp_session_step(s, nullptr, nullptr, &d);
+    if (rc != ICP_HIP_OK) break;
+    const auto t1 = std::chrono::steady_clock::now();
+    step_ms[n] = std::chrono::duration<double, std::milli>(t1 - t0).count();
+    t0 = t1;
     n++;
   }
   if (steps_done) *steps_done = n;

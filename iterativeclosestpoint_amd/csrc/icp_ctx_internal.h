@@ -16,7 +16,7 @@ struct icp_hip_ctx {
   hipEvent_t ev_it0 = nullptr, ev_it1 = nullptr;  // set_target timing
   // per-iterate timing events, a ring over the last kTimingRing iterates:
   // [0] iterate start, [1] search start, [2] search kernel done, [3] iterate end
-  static constexpr int kTimingRing = 64;
+  static constexpr int kTimingRing = 256;
   hipEvent_t ring[kTimingRing][4] = {};
   int64_t n_iterates = 0;
 

@@ -13,6 +13,9 @@
 #include <math.h>
 #include <stdlib.h>
 #include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
 
 typedef struct orc_node {
   double min_x, max_x, min_y, max_y, min_z, max_z; /* octree.h:12 */
@@ -248,13 +251,35 @@ static double point_dist(const double* a, const double* b) {
   return sqrt(dx * dx + dy * dy + dz * dz);
 }
 
+/* The queries are independent (icpengine.cpp:169-184 runs them one after another); OpenMP splits
+ * them over threads, which changes no query's result. The work counters are summed per thread. */
 void orc_nn_batch(const orc_tree* t, const double* q, int64_t n, double init_best, int32_t* idx_out,
                   double* d_out, int64_t* visits, int64_t* scanned) {
+  int64_t v = 0, sc = 0;
+#pragma omp parallel for schedule(dynamic, 1024) reduction(+ : v, sc)
   for (int64_t i = 0; i < n; i++) {
-    int32_t id = orc_find_nearest(t, q + 3 * i, init_best, visits, scanned);
+    int32_t id = orc_find_nearest(t, q + 3 * i, init_best, &v, &sc);
     if (idx_out) idx_out[i] = id;
     if (d_out) d_out[i] = (t->n > 0) ? point_dist(q + 3 * i, t->pts + 3 * (int64_t)id) : 0.0;
   }
+  if (visits) *visits += v;
+  if (scanned) *scanned += sc;
+}
+
+void orc_set_threads(int n) {
+#ifdef _OPENMP
+  if (n > 0) omp_set_num_threads(n);
+#else
+  (void)n;
+#endif
+}
+
+int orc_get_threads(void) {
+#ifdef _OPENMP
+  return omp_get_max_threads();
+#else
+  return 1;
+#endif
 }
 
 /* ---------------- Eigen JacobiSVD<Matrix3d> restatement ---------------- */

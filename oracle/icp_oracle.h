@@ -53,6 +53,10 @@ int32_t orc_find_nearest(const orc_tree* t, const double q[3], double init_best,
 void orc_nn_batch(const orc_tree* t, const double* q, int64_t n, double init_best,
                   int32_t* idx_out, double* d_out, int64_t* visits, int64_t* scanned);
 
+/* OpenMP threads of the NN loop (results do not depend on it). 0/negative: unchanged. */
+void orc_set_threads(int n);
+int orc_get_threads(void);
+
 /* Eigen-style JacobiSVD of a 3x3 (row-major in/out): H = U diag(S) V^T. */
 void orc_jacobi_svd3(const double H[9], double U[9], double S[3], double V[9]);
 

@@ -79,11 +79,22 @@ def oracle() -> C.CDLL:
         L.orc_jacobi_svd3.argtypes = [_P, _P, _P, _P]
         L.orc_best_fit.argtypes = [_P, _P, C.c_int64, _P]
         L.orc_transform.argtypes = [_P, _P, C.c_int64]
+        L.orc_set_threads.argtypes = [C.c_int]
+        L.orc_get_threads.restype = C.c_int
         L.orc_icp.restype = C.c_int
         L.orc_icp.argtypes = [C.POINTER(OrcParams), _P, C.c_int64, _P, C.c_int64, C.POINTER(OrcResult),
                               C.POINTER(OrcIter), C.c_int32]
         _O = L
     return _O
+
+
+def set_threads(n: int) -> None:
+    """OpenMP threads of the oracle's NN loop (per-query results are independent of it)."""
+    oracle().orc_set_threads(int(n))
+
+
+def get_threads() -> int:
+    return int(oracle().orc_get_threads())
 
 
 def reference_available() -> bool:

@@ -4,8 +4,8 @@
   LAS pair: its outputs are checked against the oracle's CLI ICP() (oracle pinned to the
   reference by tests/test_oracle_golden.py) and the reference-pinned LAS writer/report;
 * config 3: a 1M<->1M pair written and read through the core LASIO rules, 50 engine iterations
-  with the 3-sigma cull, compared with the oracle on a 100k stride sample of the same flow and
-  with the known motion at full size.
+  with the 3-sigma cull, compared with the CPU oracle on the same full-size flow (transform RMSE
+  <= 1e-6) and with the known motion.
 """
 from __future__ import annotations
 
@@ -94,18 +94,21 @@ def test_config3_las_pair_engine_50_iterations(icp, oracle, tmp_path):
     t_in, _ = _lib.las_read(tmp_path / "tgt.las", _lib.LAS_CORE)
     assert s_in.shape == src.shape and hs.num_points == len(src)
     assert np.max(np.abs(s_in - src)) <= 0.001 * (1 + 1e-9)
-    p = icp.params_default(max_iterations=50)
+    p = icp.params_default(max_iterations=50, tolerance=0.0)  # all 50 iterations run
     rc, res, hist, _ = icp.engine_register(p, s_in, t_in, device=0)
-    assert rc == 0 and res.success
+    assert rc == 0 and res.success and res.total_iterations == 50
     assert all(h.outlier_points > 0 for h in hist[1:])  # the cull is active (1% outliers injected)
     T = _Tres(res)
     np.testing.assert_allclose(T[:3, :3], T_true[:3, :3], atol=2e-4)
     np.testing.assert_allclose(T[:3, 3], T_true[:3, 3], atol=2e-3)
-    # the same flow on a 100k stride sample against the oracle (engine rules)
-    ss, ts = s_in[::10], t_in[::10]
-    rc, res_g, hist_g, _ = icp.engine_register(p, ss, ts, device=0)
-    orc, ores, ohist, _ = oracle.icp(ss, ts, oracle.SEM_ENGINE, 50, p.tolerance)
-    assert rc == 0 and orc == 0
-    assert res_g.total_iterations == ores.total_iterations
-    assert [h.valid_points for h in hist_g] == [h.valid for h in ohist]
-    np.testing.assert_allclose(_Tres(res_g), _Tres(ores), atol=1e-10)
+    # the whole flow on the CPU oracle (engine rules, OpenMP NN loop), full 1M <-> 1M, 50 iterations:
+    # equal iteration count and per-iteration valid counts, final transform within the north
+    # star's 1e-6 RMSE (observed ~1e-15), final RMSE to 1e-9 relative
+    orc, ores, ohist, o_out = oracle.icp(s_in, t_in, oracle.SEM_ENGINE, 50, p.tolerance)
+    assert orc == 0
+    assert res.total_iterations == ores.total_iterations
+    assert [h.valid_points for h in hist] == [h.valid for h in ohist]
+    To = _Tres(ores)
+    assert float(np.sqrt(np.mean((T - To) ** 2))) <= 1e-6
+    np.testing.assert_allclose(T, To, atol=1e-9)
+    np.testing.assert_allclose(res.final_rmse, ores.final_rmse, rtol=1e-9)

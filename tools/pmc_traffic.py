@@ -2,8 +2,10 @@
 """Summarise rocprofv3 output of the bench into profiles/ (HBM traffic per search launch).
 
 Reads the kernel-trace stats and the counter-collection CSVs written by tools/profile_bench.sh
-and applies the gfx950 correction of MI355X_MICROARCH.md §HBM: FETCH_SIZE/WRITE_SIZE are KiB;
-FETCH_SIZE reports 1/2 of the bytes of wide (16 B/lane) reads, so reads are doubled.
+and applies the read/write factors calibrated for the search kernel's own access widths by
+tools/calib_pmc.sh (profiles/calibration.json: 8-B/lane streams and 24-of-32-B / 56-of-64-B record
+gathers all read as 1/2 of the true bytes in FETCH_SIZE; stores read exactly in WRITE_SIZE).
+FETCH_SIZE/WRITE_SIZE are KiB and count L2 <-> fabric traffic (Infinity-Cache hits included).
 
 usage: pmc_traffic.py PROF_DIR N WORLD  -> JSON on stdout
 """
@@ -13,7 +15,19 @@ import json
 import sys
 from collections import defaultdict
 
-KERNEL = "k_nn4<true"
+KERNEL = "k_nn_wave<true"
+
+
+def _factors():
+    import json as _j
+    from pathlib import Path as _P
+    c = _j.loads((_P(__file__).resolve().parents[1] / "profiles" / "calibration.json").read_text())["patterns"]
+    reads = [c[k]["read_factor"] for k in ("k_stream8", "k_gather32", "k_gather64")]
+    writes = [c[k]["write_factor"] for k in ("k_store8", "k_store4")]
+    return sum(reads) / len(reads), sum(writes) / len(writes)
+
+
+READ_FACTOR, WRITE_FACTOR = _factors()
 
 
 def rows(pattern):
@@ -35,11 +49,10 @@ def per_dispatch(prof, sub):
 
 def main():
     prof, n, world = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
-    import hashlib
     from pathlib import Path
-    src = Path(__file__).resolve().parents[1] / "iterativeclosestpoint_amd" / "csrc" / "kernels.hip"
-    out = {"kernel": KERNEL, "n": n, "world": world,
-           "kernels_hip_sha1": hashlib.sha1(src.read_bytes()).hexdigest()}
+    sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+    from bench import search_source_sha1
+    out = {"kernel": KERNEL, "n": n, "world": world, "search_src_sha1": search_source_sha1()}
     stats = rows(f"{prof}/trace/**/*kernel_stats.csv")
     for r in stats:
         if KERNEL in r.get("Name", r.get("KernelName", "")):
@@ -52,13 +65,15 @@ def main():
     hits = per_dispatch(prof, "pmc_l2")
     if fetch:
         out["fetch_size_kib_raw"] = fetch[0]
-        out["fetch_bytes_corrected"] = fetch[0] * 1024 * 2
+        out["read_factor"] = READ_FACTOR
+        out["fetch_bytes_corrected"] = fetch[0] * 1024 * READ_FACTOR
         out["pmc_dispatches"] = fetch[1]
     if write:
         out["write_size_kib_raw"] = write[0]
-        out["write_bytes"] = write[0] * 1024
+        out["write_factor"] = WRITE_FACTOR
+        out["write_bytes"] = write[0] * 1024 * WRITE_FACTOR
     if fetch and write:
-        out["hbm_bytes_per_launch"] = out["fetch_bytes_corrected"] + out["write_bytes"]
+        out["bytes_per_launch"] = out["fetch_bytes_corrected"] + out["write_bytes"]
     if "TCC_HIT_sum" in hits and "TCC_MISS_sum" in hits:
         h, m = hits["TCC_HIT_sum"][0], hits["TCC_MISS_sum"][0]
         out["l2_hit_rate"] = h / (h + m) if h + m else None

@@ -15,7 +15,7 @@ for r in rows:
 for k, v in sorted(per.items(), key=lambda kv: -sum(kv[1])):
     v2 = sorted(v)
     print(f"{len(v):4d} x  median {v2[len(v2) // 2]:9.1f} us  total {sum(v):10.1f}  {k}")
-starts = [i for i, r in enumerate(rows) if "k_nn4" in r["Kernel_Name"]]
+starts = [i for i, r in enumerate(rows) if "k_nn_wave" in r["Kernel_Name"]]
 if len(starts) >= 3:
     a, b = starts[-3], starts[-2]  # one full iteration (the last one is the untimed probe)
     t0 = int(rows[a]["Start_Timestamp"])
