@@ -203,6 +203,9 @@ def main() -> int:
     ap.add_argument("--exchange", choices=("rccl", "host"), default="rccl",
                     help="per-iteration all-gathers: RCCL (default), or over torch.distributed gloo "
                          "through the host (rehearsal of N ranks on one GPU; RCCL refuses that)")
+    ap.add_argument("--rccl-self", action="store_true",
+                    help="one rank: run the iterations over a 1-rank RCCL communicator (the multi-rank "
+                         "path: ncclAllGather + rank-order device merges) instead of the plain path")
     ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "traffic_latest.json"),
                     help="PMC-derived bytes per search launch (written by tools/pmc_traffic.py)")
     args = ap.parse_args()
@@ -243,6 +246,8 @@ def main() -> int:
         uid = [icp.Context.unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         ctx.comm_init(world, rank, uid[0])
+    elif args.rccl_self:
+        ctx.comm_init(1, 0, icp.Context.unique_id())
     setup_s = time.perf_counter() - t_setup
     build_on_dev, build_ms = ctx.target_build_info()
 
@@ -332,7 +337,8 @@ def main() -> int:
                             f"source sharded over {world} rank(s) on {gpus_used} GPU(s), target octree replicated",
                 "n_target": n, "n_source": n, "ranks": world, "ranks_per_gpu": world // gpus_used,
                 "parallelism": f"spatial source shards x{world} (kd-order ranges; "
-                + ("RCCL" if args.exchange == "rccl" else "host/gloo rehearsal") + " all-gather of 2 moment records per iteration)",
+                + ("RCCL" if args.exchange == "rccl" else "host/gloo rehearsal") + " all-gather of 2 moment records per iteration)"
+                + ("; 1-rank RCCL communicator (multi-rank path)" if world == 1 and args.rccl_self else ""),
                 "octree_nodes": info["n_nodes"], "octree_leaves": info["n_leaves"],
             },
             "median": {"iter_ms": round(med_ms, 4), "value": round(n / med_ms / 1e3, 3),

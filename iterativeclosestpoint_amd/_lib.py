@@ -23,7 +23,6 @@ DBG_SLOTS = 24
 # icp_hip.h ICP_DBG_* slot names
 DBG_NAMES = {0: "waves", 1: "overflow_waves", 2: "not_joined", 3: "not_covered", 4: "rescan_points",
              5: "walk_batches", 6: "no_guess", 7: "candidates", 14: "ball_overflow", 15: "ball_points",
-             16: "clk_guess", 17: "clk_walk", 18: "clk_scan", 19: "clk_finish", 20: "clk_start",
              21: "start_nodes"}
 
 _P = C.c_void_p

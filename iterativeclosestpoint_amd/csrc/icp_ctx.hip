@@ -107,6 +107,7 @@ static NNLaunch base_launch(const icp_hip_ctx* c) {
   a.cells = c->cells;
   a.cell_lmax = c->cell_lmax;
   a.join_factor = c->cfg.join_factor;
+  a.neg_inf = -__builtin_inff();
   a.dbg = c->dbg;
   for (int k = 0; k < 3; k++) {
     a.root_lo[k] = c->root_box[k];

@@ -54,6 +54,7 @@ struct NNLaunch {
   double root_lo[3], root_hi[3];  // root box (the octree's midpoint recursion starts here)
   unsigned long long* dbg;  // optional diagnostics of the wave search (ICP_DBG_* slots)
   double join_factor;       // a lane joins the wave box if its radius <= this x the mean radius
+  float neg_inf;            // -inf (a launch value: an operand the compiler cannot fold)
 };
 
 // Threads per block of the per-thread search kernels for a given stack depth.

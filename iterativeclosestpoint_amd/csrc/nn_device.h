@@ -54,6 +54,12 @@ __device__ __forceinline__ double lane63_d(double v) {
   const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(b >> 32), 63);
   return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
+__device__ __forceinline__ double readlane_d(double v, int lane) {
+  const long long b = __double_as_longlong(v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)b, lane);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(b >> 32), lane);
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
 __device__ __forceinline__ double wave_sum_d(double v) {
   v += dpp_d<0x111, 0xf, true>(v);
   v += dpp_d<0x112, 0xf, true>(v);
@@ -83,6 +89,45 @@ __device__ __forceinline__ double wave_max_d(double v) {
   v = dmax_(v, dpp_d<0x143, 0xc, false>(v));
   return lane63_d(v);
 }
+// 32-bit wave reductions: row shifts then row broadcasts, each step one DPP-combined VALU
+// instruction (the old operand is the operation's identity, so the compiler folds the move).
+__device__ __forceinline__ int wave_min_i(int v) {
+  constexpr int I = 0x7fffffff;
+  v = min(v, __builtin_amdgcn_update_dpp(I, v, 0x111, 0xf, 0xf, false));
+  v = min(v, __builtin_amdgcn_update_dpp(I, v, 0x112, 0xf, 0xf, false));
+  v = min(v, __builtin_amdgcn_update_dpp(I, v, 0x114, 0xf, 0xf, false));
+  v = min(v, __builtin_amdgcn_update_dpp(I, v, 0x118, 0xf, 0xf, false));
+  v = min(v, __builtin_amdgcn_update_dpp(I, v, 0x142, 0xa, 0xf, false));
+  v = min(v, __builtin_amdgcn_update_dpp(I, v, 0x143, 0xc, 0xf, false));
+  return __builtin_amdgcn_readlane(v, 63);
+}
+__device__ __forceinline__ int wave_max_i(int v) {
+  constexpr int I = (int)0x80000000;
+  v = max(v, __builtin_amdgcn_update_dpp(I, v, 0x111, 0xf, 0xf, false));
+  v = max(v, __builtin_amdgcn_update_dpp(I, v, 0x112, 0xf, 0xf, false));
+  v = max(v, __builtin_amdgcn_update_dpp(I, v, 0x114, 0xf, 0xf, false));
+  v = max(v, __builtin_amdgcn_update_dpp(I, v, 0x118, 0xf, 0xf, false));
+  v = max(v, __builtin_amdgcn_update_dpp(I, v, 0x142, 0xa, 0xf, false));
+  v = max(v, __builtin_amdgcn_update_dpp(I, v, 0x143, 0xc, 0xf, false));
+  return __builtin_amdgcn_readlane(v, 63);
+}
+__device__ __forceinline__ float wave_sum_f(float v) {
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x111, 0xf, 0xf, true));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x112, 0xf, 0xf, true));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x114, 0xf, 0xf, true));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x118, 0xf, 0xf, true));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x142, 0xa, 0xf, false));
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x143, 0xc, 0xf, false));
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+// Order-preserving map of non-NaN floats to int32 (and back: the map is an involution), so that
+// float min/max reductions run as integer DPP min/max.
+__device__ __forceinline__ int fkey(float f) {
+  const int b = __float_as_int(f);
+  return b ^ ((b >> 31) & 0x7fffffff);
+}
+__device__ __forceinline__ float funkey(int k) { return __int_as_float(k ^ ((k >> 31) & 0x7fffffff)); }
+
 // Inclusive prefix sum over the wave's lanes; *total = the wave's sum (uniform).
 __device__ __forceinline__ int wave_incl_scan(int v, int* total) {
   v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, true);

@@ -89,6 +89,32 @@ constexpr int kWavePoints = 1024;  // candidate points per wave
 constexpr int kWaveLds = kWaveQueue * 4 + kWavePoints * 4;  // 5 KB per wave
 static_assert(kWaveQueue * 4 >= 64 * 16 && kWaveQueue * 4 >= 32 * 32, "staging area aliases the stack");
 
+// Upper bound of sqrt(e2) (a displacement; e2 >= 0) from the fp32 square root: (float) rounds by
+// <= 2^-24, v_sqrt_f32 is within 1 ulp, each fp32 product by <= 2^-24; 2^-60 covers e2 below the
+// fp32 normal range. Overflow gives +inf (the lane then has no usable guess).
+__device__ __forceinline__ double disp_upper(double e2) {
+  const float s = __builtin_sqrtf((float)e2 * (1.0f + 0x1p-21f)) * (1.0f + 0x1p-21f) + 0x1p-60f;
+  return (double)s;
+}
+
+// fp32 radius r >= sqrt(u) (1 + 2^-40) + amax 2^-45 (the ball of the wave search's certificate):
+// the fp32 square root rounded up as in disp_upper, the amax term doubled, 2^-49 absolute for u
+// below the fp32 normal range, and the sum's rounding covered by the 2^-21 factors.
+__device__ __forceinline__ float ball_radius32(double u, double amax) {
+  const float s = __builtin_sqrtf((float)u * (1.0f + 0x1p-21f)) * (1.0f + 0x1p-21f);
+  return s + ((float)(amax * 0x1p-44) + 0x1p-49f);
+}
+
+// fp64 box bound o + f rounded down / up (the addition rounds by <= 2^-53 of the result).
+__device__ __forceinline__ double box_lo(double o, float f) {
+  const double b = o + (double)f;
+  return b - (__builtin_fabs(b) * 0x1p-52 + 0x1p-1000);
+}
+__device__ __forceinline__ double box_hi(double o, float f) {
+  const double b = o + (double)f;
+  return b + (__builtin_fabs(b) * 0x1p-52 + 0x1p-1000);
+}
+
 // Lower bound of fl64(d2) of every point whose fp32 squared distance (the scan) is >= s32.
 // Coordinates are offsets from B's centre, |offset| <= ext for points and joined queries. With
 // u = 2^-24: each fp32 offset differs from the exact one by <= ext (u + 2^-53) =: ext k; the fp32
@@ -101,10 +127,13 @@ __device__ __forceinline__ double scan32_lower_bound(float s32, double ext) {
   if (!(s32 < __builtin_inff())) return __builtin_inf();
   const double u = 0x1p-24;
   const double e_abs = 1.7320509 * 2.0 * ext * (u * (1.0 + 0x1p-20)) * (1.0 + u) * (1.0 + 0x1p-40);
-  double n2 = ((double)s32 - 0x1p-120) / (1.0 + 3.0001 * u);
+  // x / (1 + a) >= x (1 - a) for x >= 0: products instead of divisions
+  const double n2 = ((double)s32 - 0x1p-120) * (1.0 - 3.0001 * u);
   if (!(n2 > 0.0)) return 0.0;
-  const double n = __builtin_sqrt(n2) * (1.0 - 0x1p-50);
-  double d = (n - e_abs) / (1.0 + u) * (1.0 - 0x1p-50);
+  // sqrt(n2) from below: (float) rounds by <= 2^-24 (scaled down first), v_sqrt_f32 is within
+  // 1 ulp, the fp64 factor covers both (a flushed denormal gives 0, still a lower bound)
+  const double n = (double)__builtin_sqrtf((float)(n2 * (1.0 - 0x1p-22))) * (1.0 - 0x1p-21);
+  const double d = (n - e_abs) * (1.0 - u) * (1.0 - 0x1p-50);
   if (!(d > 0.0)) return 0.0;
   return d * d * (1.0 - 0x1p-48);
 }
@@ -113,7 +142,7 @@ template <bool APPLY>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) k_nn_wave(NNLaunch a) {
   extern __shared__ __attribute__((aligned(16))) unsigned long long lds_raw[];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int32_t i = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);  // n <= INT32_MAX (set_source)
   const bool active = i < a.n;
   unsigned char* wl = reinterpret_cast<unsigned char*>(lds_raw) + wv * kWaveLds;
   int32_t* queue = reinterpret_cast<int32_t*>(wl);
@@ -129,13 +158,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
   load_query<APPLY>(a, i, active, qx, qy, qz);
   const bool finite_q = __builtin_isfinite(qx) && __builtin_isfinite(qy) && __builtin_isfinite(qz);
 
-  const unsigned long long t_p0 = a.dbg ? __builtin_amdgcn_s_memtime() : 0ull;
   // Phase 1: the guess (any value is safe: certification also requires best <= u).
   double u = __builtin_inf();
   if (active && finite_q && a.have_prev) {
     const double dp = a.dist_out[i];
     const double ex = qx - ox, ey = qy - oy, ez = qz - oz;
-    const double g = dp + __builtin_sqrt(ex * ex + ey * ey + ez * ez);
+    const double g = dp + disp_upper(ex * ex + ey * ey + ez * ez);
     u = (g * g) * (1.0 + 0x1p-30);
   } else if (active && finite_q) {
     const NodeRec* r0 = a.nodes;
@@ -178,22 +206,42 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
     }
   }
 
-  // Phase 2: the wave's search box over the lanes that join.
-  const bool cand = active && finite_q && u <= 0x1p900;
+  // Phase 2: the wave's search box over the lanes that join. Every point with fl(d2) <= u (1 +
+  // 2^-47) lies within r of the query, r >= sqrt(u) (1 + 2^-40) + |q|_max 2^-45 (ball_radius32).
+  // B may be any box that holds the joined balls: it is reduced in fp32 relative to the first
+  // joined query o, rounded outwards, and converted back to fp64 rounded outwards.
   const double amax = __builtin_fmax(__builtin_fabs(qx), __builtin_fmax(__builtin_fabs(qy), __builtin_fabs(qz)));
-  const double r = cand ? __builtin_sqrt(u) * (1.0 + 0x1p-40) + amax * 0x1p-45 : 0.0;
+  // |q| <= 2^100 keeps every fp32 offset of the wave finite
+  const bool cand = active && finite_q && u <= 0x1p900 && amax <= 0x1p100;
+  const float r = cand ? ball_radius32(u, amax) : 0.f;
   const unsigned long long cmask = __ballot(cand);
-  const double mean_r = wave_sum_d(r) / (double)(cmask ? __popcll(cmask) : 1);
-  bool join = cand && r <= a.join_factor * mean_r;
-  const double blx = wave_min_d(join ? qx - r : __builtin_inf());
-  const double bly = wave_min_d(join ? qy - r : __builtin_inf());
-  const double blz = wave_min_d(join ? qz - r : __builtin_inf());
-  const double bhx = wave_max_d(join ? qx + r : -__builtin_inf());
-  const double bhy = wave_max_d(join ? qy + r : -__builtin_inf());
-  const double bhz = wave_max_d(join ? qz + r : -__builtin_inf());
+  // the join rule is a heuristic (any subset may join): fp32 mean
+  const float mean_r = wave_sum_f(r) * __builtin_amdgcn_rcpf((float)(cmask ? __popcll(cmask) : 1));
+  bool join = cand && r <= (float)a.join_factor * mean_r;
+  double blx = 0.0, bly = 0.0, blz = 0.0, bhx = -1.0, bhy = -1.0, bhz = -1.0;
+  {
+    const unsigned long long jm = __ballot(join);
+    if (jm != 0) {
+      const int ol = __builtin_ctzll(jm);
+      const double ox_ = readlane_d(qx, ol), oy_ = readlane_d(qy, ol), oz_ = readlane_d(qz, ol);
+      float lo[3], hi[3];
+      const double dq[3] = {qx - ox_, qy - oy_, qz - oz_};
+#pragma unroll
+      for (int k = 0; k < 3; k++) {
+        const float d = (float)dq[k];
+        const float m = (__builtin_fabsf(d) + r) * 0x1p-21f + 0x1p-126f;
+        lo[k] = join ? (d - r) - m : __builtin_inff();
+        hi[k] = join ? (d + r) + m : -__builtin_inff();
+      }
+      blx = box_lo(ox_, funkey(wave_min_i(fkey(lo[0]))));
+      bly = box_lo(oy_, funkey(wave_min_i(fkey(lo[1]))));
+      blz = box_lo(oz_, funkey(wave_min_i(fkey(lo[2]))));
+      bhx = box_hi(ox_, funkey(wave_max_i(fkey(hi[0]))));
+      bhy = box_hi(oy_, funkey(wave_max_i(fkey(hi[1]))));
+      bhz = box_hi(oz_, funkey(wave_max_i(fkey(hi[2]))));
+    }
+  }
 
-  const unsigned long long t_p2 = a.dbg ? __builtin_amdgcn_s_memtime() : 0ull;
-  unsigned long long t_pd = t_p2;
   // Phase 3: the leaves meeting B.
   int nleaf = 0;
   bool overflow = false;
@@ -220,7 +268,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
       }
       if (lane == 0) queue[0] = start;
     }
-    if (a.dbg) t_pd = __builtin_amdgcn_s_memtime();
     // Every batch pops up to 64 nodes, which already meet B (tested by their parent; the start
     // nodes by the cell box or the descent), appends the points of its leaves to the candidate
     // list and pushes its children meeting B. Most recent first: the live set stays small.
@@ -274,7 +321,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
     if (overflow) atomicAdd(&a.dbg[1], 1ull);
   }
 
-  const unsigned long long t_p3 = a.dbg ? __builtin_amdgcn_s_memtime() : 0ull;
   // Phase 4: the lockstep scan: 64 candidates per chunk are gathered by one load per lane (the
   // next chunk's gather is in flight while the current one is scanned from LDS).
   double best = __builtin_inf(), second = __builtin_inf();
@@ -291,7 +337,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
       // staging area: points in pairs, [x0 x1 y0 y1 z0 z1 w0 w1] (32 B), so that one packed fp32
       // instruction (v_pk_add/mul/fma_f32) evaluates an axis of two points
       float* stage32 = reinterpret_cast<float*>(wl);
-      float s1 = __builtin_inff(), s2 = __builtin_inff();
+      // Selection keys: the fp32 squared distance with its low 6 bits replaced by the point's slot
+      // in the chunk (v_bfi), so that the two smallest are kept by two med3 per point and the
+      // winner is found from its slot once per chunk. A key is within 63 ulps of its value, and
+      // s2 & ~63 is a lower bound of the second-smallest value; keys are finite and >= 0 (offsets
+      // <= ext <= 2^60, pads far but finite), so float order is key order.
+      const float ninf = a.neg_inf;  // -inf from the launch record: an opaque med3 operand
+      float k1 = __builtin_inff(), k2 = __builtin_inff();
       int32_t p1 = -1;
       wave_lds_fence();
       double4 nxtp = make_double4(0.0, 0.0, 0.0, 0.0);
@@ -318,12 +370,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
           sp[6] = vw;
         }
         if ((m & 1) && lane == 63) {
-          // odd count: the last pair's second point at +inf (its sq = +inf never replaces s1 and
-          // leaves s2 unchanged; no NaN can arise from inf - finite)
+          // odd count: the last pair's second point far away (finite: its key never wins and
+          // never becomes the second smallest of a lane that scanned a real point)
           float* sp = stage32 + 8 * (m >> 1) + 1;
-          sp[0] = __builtin_inff();
-          sp[2] = __builtin_inff();
-          sp[4] = __builtin_inff();
+          sp[0] = 0x1p60f;
+          sp[2] = 0x1p60f;
+          sp[4] = 0x1p60f;
         }
         wave_lds_fence();
         const int nb = base + 64;
@@ -334,36 +386,42 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
           nxtp = make_double4(xy.x, xy.y, p->z, __longlong_as_double((long long)g));
         }
         scanned_pts += m;
-        // lockstep over the staged pairs (16-B broadcast reads). Point 2k is selected before point
-        // 2k + 1: the same sequence of updates as a one-point-at-a-time scan.
+        // lockstep over the staged pairs (16-B broadcast reads); one packed instruction evaluates
+        // an axis of two points
         typedef float f2 __attribute__((ext_vector_type(2)));
         typedef int v4i __attribute__((ext_vector_type(4)));
         const f2 qx2 = {qx32, qx32}, qy2 = {qy32, qy32}, qz2 = {qz32, qz32};
-        auto sel = [&](float sq, int w) {
-          const bool lt = sq < s1;
-          s2 = __builtin_amdgcn_fmed3f(s1, s2, sq);
-          s1 = lt ? sq : s1;
-          p1 = lt ? w : p1;
+        const float k1_in = k1;
+        auto sel = [&](float sq, uint32_t sl) {
+          const float key = __uint_as_float((sl & 63u) | (__float_as_uint(sq) & ~63u));
+          k2 = __builtin_amdgcn_fmed3f(k1, k2, key);
+          k1 = __builtin_amdgcn_fmed3f(k1, key, ninf);
         };
-        auto eval2 = [&](const v4i xy, const v4i zw) {
+        auto eval2 = [&](const v4i xy, const v4i zw, uint32_t sl) {
           const f2 X = {__int_as_float(xy.x), __int_as_float(xy.y)};
           const f2 Y = {__int_as_float(xy.z), __int_as_float(xy.w)};
           const f2 Z = {__int_as_float(zw.x), __int_as_float(zw.y)};
           const f2 dx = X - qx2, dy = Y - qy2, dz = Z - qz2;
           const f2 sq = __builtin_elementwise_fma(dz, dz, __builtin_elementwise_fma(dy, dy, dx * dx));
-          sel(sq.x, zw.z);
-          sel(sq.y, zw.w);
+          sel(sq.x, sl);
+          sel(sq.y, sl + 1u);
         };
         const v4i* st4 = reinterpret_cast<const v4i*>(stage32);
         const int mp = (m + 1) >> 1;
         int k = 0;
         for (; k + 2 <= mp; k += 2) {
           const v4i a0 = st4[2 * k], b0 = st4[2 * k + 1], a1 = st4[2 * k + 2], b1 = st4[2 * k + 3];
-          eval2(a0, b0);
-          eval2(a1, b1);
+          eval2(a0, b0, 2u * k);
+          eval2(a1, b1, 2u * k + 2u);
         }
-        if (k < mp) eval2(st4[2 * k], st4[2 * k + 1]);
+        if (k < mp) eval2(st4[2 * k], st4[2 * k + 1], 2u * k);
+        // the winner of this chunk, if it improved the lane's best: its index from its slot
+        if (k1 != k1_in) {
+          const uint32_t sl = __float_as_uint(k1) & 63u;
+          p1 = __float_as_int(stage32[8 * (sl >> 1) + 6 + (sl & 1u)]);
+        }
       }
+      const float s2 = __uint_as_float(__float_as_uint(k2) & ~63u);  // <= the second-smallest value
       // fp64 distance of the fp32 winner, exactly as the leaf scan computes it (octree.cpp:139-144)
       double b64 = __builtin_inf();
       if (join && p1 >= 0) {
@@ -372,8 +430,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
         b64 = dx * dx + dy * dy + dz * dz;
       }
       const double lb2 = scan32_lower_bound(s2, ext);
-      // a lane whose fp32 winner is not within its guess goes to the per-lane search either way
-      const bool ok = !join || p1 < 0 || !(b64 <= u) || certified(b64, lb2, a.init_best);
+      // Decided lanes: nothing scanned; every point beyond the guess (the fp32 winner and the
+      // bound of the rest: the per-lane search takes it, as after an fp64 scan); or a certified
+      // winner within the guess. Anything else (a near tie, or a winner beyond u while another
+      // point may be within it) re-scans the wave in fp64, which decides as the fp64 scan does.
+      const bool ok = !join || p1 < 0 || (!(b64 <= u) && lb2 > u) || (b64 <= u && certified(b64, lb2, a.init_best));
       if (__ballot(!ok) == 0) {
         best = b64;
         second = lb2;
@@ -443,7 +504,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
     }
   }
 
-  const unsigned long long t_p4 = a.dbg ? __builtin_amdgcn_s_memtime() : 0ull;
   // Phase 5: certify, write, or queue.
   bool written = false, to_exact = false, to_lane = false;
   double d = 0.0;
@@ -472,14 +532,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
   wave_append(to_exact, i, a.fb_count, a.fb_list);
   const bool covered = !(join && !(best <= u));
   wave_append_u(to_lane, i, covered ? u : __builtin_inf(), a.fb_count + 1, a.fb_list2, a.fb_u2);
-  if (a.dbg && lane == 0) {
-    const unsigned long long t_p5 = __builtin_amdgcn_s_memtime();
-    atomicAdd(&a.dbg[16], t_p2 - t_p0);
-    atomicAdd(&a.dbg[17], t_p3 - t_pd);
-    atomicAdd(&a.dbg[20], t_pd - t_p2);
-    atomicAdd(&a.dbg[18], t_p4 - t_p3);
-    atomicAdd(&a.dbg[19], t_p5 - t_p4);
-  }
 }
 
 // ---------------------------------------------------------------------------------------------
