@@ -206,6 +206,8 @@ def main() -> int:
     ap.add_argument("--rccl-self", action="store_true",
                     help="one rank: run the iterations over a 1-rank RCCL communicator (the multi-rank "
                          "path: ncclAllGather + rank-order device merges) instead of the plain path")
+    ap.add_argument("--config", action="append", default=[], metavar="KEY=VALUE",
+                    help="icp_hip_config field for the context (A/B of search options), repeatable")
     ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "traffic_latest.json"),
                     help="PMC-derived bytes per search launch (written by tools/pmc_traffic.py)")
     args = ap.parse_args()
@@ -230,7 +232,11 @@ def main() -> int:
     t_setup = time.perf_counter()
     tgt, src, T_true = icp.synth_pair(n)
     lo, hi = shard_range(n, rank, world)
-    ctx = icp.Context(device)
+    conf = None
+    if args.config:
+        kv = dict(c.split("=", 1) for c in args.config)
+        conf = icp.config(**{k: (float(v) if "." in v else int(v)) for k, v in kv.items()})
+    ctx = icp.Context(device, conf)
     ctx.set_target(tgt, 10, 20, icp.RULES_ENGINE)
     # spatial shards: contiguous ranges of the kd order (a contiguous range of the shuffled cloud
     # would thin each rank's queries `world` times; see icp_host.h icp_source_shard_order)

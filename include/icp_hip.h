@@ -63,7 +63,10 @@ typedef struct icp_hip_config {
   double join_factor;     /* a query joins its wave's search box if its search radius is at most
                              join_factor x the wave's mean radius                      default 3.0 */
   int32_t debug_counters; /* 1: the wave search counts its phases (icp_hip_debug_counters) dflt 0 */
-  int32_t reserved[7];    /* zero */
+  int32_t xcd_blocks;     /* > 0: the wave search's blocks are renumbered so that each XCD (own
+                             L2) takes runs of this many consecutive (spatially adjacent)
+                             blocks, dealt round-robin over the XCDs; 0: hardware order  dflt 256 */
+  int32_t reserved[6];    /* zero */
 } icp_hip_config;
 
 /* Slots of icp_hip_debug_counters (summed over the last iterate's search launches). */

@@ -55,6 +55,7 @@ struct NNLaunch {
   unsigned long long* dbg;  // optional diagnostics of the wave search (ICP_DBG_* slots)
   double join_factor;       // a lane joins the wave box if its radius <= this x the mean radius
   float neg_inf;            // -inf (a launch value: an operand the compiler cannot fold)
+  int xcd_blocks;           // renumber the wave search's blocks XCD-contiguously
 };
 
 // Threads per block of the per-thread search kernels for a given stack depth.

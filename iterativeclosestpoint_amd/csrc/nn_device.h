@@ -531,14 +531,14 @@ __device__ __forceinline__ uint32_t axis_path(double v, double lo, double hi, in
 }
 
 // Start nodes of a box query from the cell tables: the cells of level L (the octree's own
-// midpoint grid) that the box [bl, bh] overlaps, one lane each. The box's cells are an index box
+// midpoint grid) that the box [bl, bh] overlaps, K per lane. The box's cells are an index box
 // [il, ih]^3, every one of them meets the box, and every target point inside the box lies in one
 // of them; the table gives the node holding all points of a cell (the depth-L node or the leaf
 // above it; a leaf spanning several cells is taken once, from its first cell in the box). L is
-// the deepest table level at which the box spans at most G cells (G = lanes of the group).
+// the deepest table level at which the box spans at most K G cells (G = lanes of the group).
 // Lanes gl < 6 of the group compute the six axis paths. Writes the start nodes to out[0..count)
 // and returns count (group-uniform). Every lane of the group must call it.
-template <int G>
+template <int G, int K>
 __device__ __forceinline__ int cell_starts(const NNLaunch& a, double blx, double bly, double blz, double bhx,
                                            double bhy, double bhz, int gl, int gbase, int32_t* out) {
   int L = a.cell_lmax;
@@ -564,35 +564,48 @@ __device__ __forceinline__ int cell_starts(const NNLaunch& a, double blx, double
     ilz = (uint32_t)__shfl((int)path, gbase + 4, kWave);
     ihz = (uint32_t)__shfl((int)path, gbase + 5, kWave);
   }
-  while (L > 0 && (ihx - ilx + 1) * (ihy - ily + 1) * (ihz - ilz + 1) > (uint32_t)G) {
+  while (L > 0 && (ihx - ilx + 1) * (ihy - ily + 1) * (ihz - ilz + 1) > (uint32_t)(K * G)) {
     L--;
     ilx >>= 1; ihx >>= 1; ily >>= 1; ihy >>= 1; ilz >>= 1; ihz >>= 1;
   }
-  const uint32_t nx = ihx - ilx + 1, ny = ihy - ily + 1, nz = ihz - ilz + 1;
-  bool put = false;
-  int32_t node = 0;
-  if ((uint32_t)gl < nx * ny * nz) {
-    const uint32_t cx = ilx + (uint32_t)gl % nx, cy = ily + ((uint32_t)gl / nx) % ny,
-                   cz = ilz + (uint32_t)gl / (nx * ny);
-    const uint32_t prefix = spread3(cx) | (spread3(cy) << 1) | (spread3(cz) << 2);
-    const int32_t e = a.cells[(((int64_t)1 << (3 * L)) - 1) / 7 + prefix];
-    if (e >= 0) {
-      node = e >> 5;
-      const int sh = L - (e & 31);
-      const uint32_t fx = ((cx >> sh) << sh) > ilx ? ((cx >> sh) << sh) : ilx;
-      const uint32_t fy = ((cy >> sh) << sh) > ily ? ((cy >> sh) << sh) : ily;
-      const uint32_t fz = ((cz >> sh) << sh) > ilz ? ((cz >> sh) << sh) : ilz;
-      put = cx == fx && cy == fy && cz == fz;
+  const uint32_t nx = ihx - ilx + 1, ny = ihy - ily + 1, nz = ihz - ilz + 1, ncell = nx * ny * nz;
+  const int64_t base = (((int64_t)1 << (3 * L)) - 1) / 7;
+  // all K table reads in flight before any is used
+  uint32_t cx[K], cy[K], cz[K];
+  int32_t e[K];
+#pragma unroll
+  for (int k = 0; k < K; k++) {
+    const uint32_t c = (uint32_t)gl + (uint32_t)(k * G);
+    e[k] = -1;
+    cx[k] = ilx + c % nx;
+    cy[k] = ily + (c / nx) % ny;
+    cz[k] = ilz + c / (nx * ny);
+    if (c < ncell) e[k] = a.cells[base + (spread3(cx[k]) | (spread3(cy[k]) << 1) | (spread3(cz[k]) << 2))];
+  }
+  int count = 0;
+#pragma unroll
+  for (int k = 0; k < K; k++) {
+    bool put = false;
+    int32_t node = 0;
+    if (e[k] >= 0) {
+      node = e[k] >> 5;
+      const int sh = L - (e[k] & 31);
+      const uint32_t fx = ((cx[k] >> sh) << sh) > ilx ? ((cx[k] >> sh) << sh) : ilx;
+      const uint32_t fy = ((cy[k] >> sh) << sh) > ily ? ((cy[k] >> sh) << sh) : ily;
+      const uint32_t fz = ((cz[k] >> sh) << sh) > ilz ? ((cz[k] >> sh) << sh) : ilz;
+      put = cx[k] == fx && cy[k] == fy && cz[k] == fz;
+    }
+    if (G == 64) {
+      const unsigned long long pm = __ballot(put);
+      if (put) out[count + mask_rank(pm)] = node;
+      count += __popcll(pm);
+    } else {
+      const uint32_t pm = (uint32_t)((__ballot(put) >> gbase) & ((1ull << G) - 1ull));
+      if (put) out[count + __builtin_popcount(pm & ((1u << gl) - 1u))] = node;
+      count += __builtin_popcount(pm);
     }
   }
-  if (G == 64) {
-    const unsigned long long pm = __ballot(put);
-    if (put) out[mask_rank(pm)] = node;
-    return __popcll(pm);
-  }
-  const uint32_t pm = (uint32_t)((__ballot(put) >> gbase) & ((1ull << G) - 1ull));
-  if (put) out[__builtin_popcount(pm & ((1u << gl) - 1u))] = node;
-  return __builtin_popcount(pm);
+  return count;
 }
 
 // Children of an inner node that meet the closed box [bl, bh] (child o spans [lo or mid,

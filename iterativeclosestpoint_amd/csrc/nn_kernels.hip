@@ -21,6 +21,17 @@
 #include "kernels.h"
 #include "nn_device.h"
 
+// Diagnostic build only (-DICP_PHASE_CLOCKS=1): per-phase s_memtime deltas of the wave search
+// summed into the debug slots 16..21 (the product build has no clock reads).
+#ifndef ICP_PHASE_CLOCKS
+#define ICP_PHASE_CLOCKS 0
+#endif
+constexpr bool kDbgCounts = !ICP_PHASE_CLOCKS;  // the clock build counts nothing (no atomics)
+#if ICP_PHASE_CLOCKS
+#define PCLK(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#else
+#define PCLK(v)
+#endif
 namespace icp {
 
 namespace {
@@ -85,6 +96,7 @@ __global__ void __launch_bounds__(256) k_nn_ref(NNLaunch a) {
 // the certificate of nn_device.h applies. Non-joined lanes go to the ball list, uncertified ones
 // to the exact list.
 constexpr int kWaveQueue = 256;  // node ids of the walk's LIFO stack (staging area after the walk)
+constexpr int kWaveStartK = 2;   // start cells per lane (up to 128 start nodes per wave)
 constexpr int kWavePoints = 1024;  // candidate points per wave
 constexpr int kWaveLds = kWaveQueue * 4 + kWavePoints * 4;  // 5 KB per wave
 static_assert(kWaveQueue * 4 >= 64 * 16 && kWaveQueue * 4 >= 32 * 32, "staging area aliases the stack");
@@ -138,11 +150,25 @@ __device__ __forceinline__ double scan32_lower_bound(float s32, double ext) {
   return d * d * (1.0 - 0x1p-48);
 }
 
+// Workgroups are dispatched round-robin over the 8 XCDs (block b runs on XCD b % 8), each with
+// its own 4 MB L2. Renumbered, XCD x takes runs of C consecutive logical blocks (C = chunk), the
+// runs dealt round-robin over the XCDs: the waves an XCD runs at a time are neighbours in the kd
+// order (their candidate points and nodes shared in its L2), and the XCDs still share the cloud
+// evenly. Blocks past the last whole round of 8 C keep their number.
+__device__ __forceinline__ unsigned xcd_block(unsigned chunk) {
+  const unsigned b = blockIdx.x, nb = gridDim.x;
+  if (chunk == 0) return b;
+  const unsigned round = 8u * chunk, full = nb / round * round;
+  if (b >= full) return b;
+  const unsigned x = b & 7u, k = b >> 3;
+  return ((k / chunk) * 8u + x) * chunk + k % chunk;
+}
+
 template <bool APPLY>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) k_nn_wave(NNLaunch a) {
   extern __shared__ __attribute__((aligned(16))) unsigned long long lds_raw[];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int32_t i = (int32_t)(blockIdx.x * blockDim.x + threadIdx.x);  // n <= INT32_MAX (set_source)
+  const int32_t i = (int32_t)(xcd_block((unsigned)a.xcd_blocks) * blockDim.x + threadIdx.x);  // n <= INT32_MAX
   const bool active = i < a.n;
   unsigned char* wl = reinterpret_cast<unsigned char*>(lds_raw) + wv * kWaveLds;
   int32_t* queue = reinterpret_cast<int32_t*>(wl);
@@ -158,6 +184,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
   load_query<APPLY>(a, i, active, qx, qy, qz);
   const bool finite_q = __builtin_isfinite(qx) && __builtin_isfinite(qy) && __builtin_isfinite(qz);
 
+  PCLK(t_p0);
   // Phase 1: the guess (any value is safe: certification also requires best <= u).
   double u = __builtin_inf();
   if (active && finite_q && a.have_prev) {
@@ -206,6 +233,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
     }
   }
 
+  PCLK(t_p1);
   // Phase 2: the wave's search box over the lanes that join. Every point with fl(d2) <= u (1 +
   // 2^-47) lies within r of the query, r >= sqrt(u) (1 + 2^-40) + |q|_max 2^-45 (ball_radius32).
   // B may be any box that holds the joined balls: it is reduced in fp32 relative to the first
@@ -242,14 +270,15 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
     }
   }
 
+  PCLK(t_p2);
   // Phase 3: the leaves meeting B.
   int nleaf = 0;
   bool overflow = false;
   if (__ballot(join) != 0) {
     int tail = 1;
     if (a.cells) {
-      tail = cell_starts<64>(a, blx, bly, blz, bhx, bhy, bhz, lane, 0, queue);
-      if (a.dbg && lane == 0) atomicAdd(&a.dbg[21], (unsigned long long)tail);
+      tail = cell_starts<64, kWaveStartK>(a, blx, bly, blz, bhx, bhy, bhz, lane, 0, queue);
+      if (kDbgCounts && a.dbg && lane == 0) atomicAdd(&a.dbg[21], (unsigned long long)tail);
     } else {
       // Wave-uniform descent to the deepest node that holds every leaf meeting B: follow the
       // only child meeting B while there is exactly one.
@@ -264,7 +293,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
         if (__builtin_popcount(kids) != 1) break;
         const uint32_t o = (uint32_t)__builtin_ctz(kids);
         start = __builtin_amdgcn_readfirstlane(topo.x + __builtin_popcount((meta & 0xffu) & ((1u << o) - 1u)));
-        if (a.dbg && lane == 0) atomicAdd(&a.dbg[21], 1ull);
+        if (kDbgCounts && a.dbg && lane == 0) atomicAdd(&a.dbg[21], 1ull);
       }
       if (lane == 0) queue[0] = start;
     }
@@ -311,16 +340,17 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
         queue[off++] = first + __builtin_popcount(mask & ((1u << o) - 1u));
       }
       tail += tot;
-      if (a.dbg && lane == 0) atomicAdd(&a.dbg[5], 1ull);
+      if (kDbgCounts && a.dbg && lane == 0) atomicAdd(&a.dbg[5], 1ull);
       wave_lds_fence();
     }
   }
   if (overflow) join = false;
-  if (a.dbg && lane == 0) {
+  if (kDbgCounts && a.dbg && lane == 0) {
     atomicAdd(&a.dbg[0], 1ull);
     if (overflow) atomicAdd(&a.dbg[1], 1ull);
   }
 
+  PCLK(t_p3);
   // Phase 4: the lockstep scan: 64 candidates per chunk are gathered by one load per lane (the
   // next chunk's gather is in flight while the current one is scanned from LDS).
   double best = __builtin_inf(), second = __builtin_inf();
@@ -490,9 +520,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
         }
       }
     }
-    if (a.dbg && lane == 0) atomicAdd(&a.dbg[4], (unsigned long long)scanned_pts);
+    if (kDbgCounts && a.dbg && lane == 0) atomicAdd(&a.dbg[4], (unsigned long long)scanned_pts);
   }
-  if (a.dbg) {
+  if (kDbgCounts && a.dbg) {
     const unsigned long long ex = __ballot(cand && !join && !overflow);
     const unsigned long long cov = __ballot(join && !(best <= u));
     const unsigned long long nc = __ballot(active && finite_q && !cand);
@@ -504,6 +534,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
     }
   }
 
+  PCLK(t_p4);
   // Phase 5: certify, write, or queue.
   bool written = false, to_exact = false, to_lane = false;
   double d = 0.0;
@@ -532,6 +563,16 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
   wave_append(to_exact, i, a.fb_count, a.fb_list);
   const bool covered = !(join && !(best <= u));
   wave_append_u(to_lane, i, covered ? u : __builtin_inf(), a.fb_count + 1, a.fb_list2, a.fb_u2);
+#if ICP_PHASE_CLOCKS
+  PCLK(t_p5);
+  if (a.dbg && lane == 0) {
+    atomicAdd(&a.dbg[16], t_p1 - t_p0);
+    atomicAdd(&a.dbg[17], t_p2 - t_p1);
+    atomicAdd(&a.dbg[18], t_p3 - t_p2);
+    atomicAdd(&a.dbg[19], t_p4 - t_p3);
+    atomicAdd(&a.dbg[20], t_p5 - t_p4);
+  }
+#endif
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -582,7 +623,7 @@ __global__ void __launch_bounds__(64) k_nn_ball(NNLaunch a) {
       const double amax = __builtin_fmax(__builtin_fabs(qx), __builtin_fmax(__builtin_fabs(qy), __builtin_fabs(qz)));
       const double r = live ? __builtin_sqrt(thr) * (1.0 + 0x1p-40) + amax * 0x1p-45 : 0.0;
       if (a.cells) {
-        const int t = cell_starts<kBallGL>(a, qx - r, qy - r, qz - r, qx + r, qy + r, qz + r, gl, gbase, stack);
+        const int t = cell_starts<kBallGL, 1>(a, qx - r, qy - r, qz - r, qx + r, qy + r, qz + r, gl, gbase, stack);
         tail = live ? t : 0;
       } else {
         if (gl == 0) stack[0] = 0;

@@ -382,9 +382,10 @@ int64_t cell_table_entries(int lmax) {
 int64_t cell_table_offset(int l) { return l == 0 ? 0 : cell_table_entries(l - 1); }
 
 int cell_table_depth(int64_t n_leaves, int max_inner_depth) {
-  // about one cell per leaf at the deepest table level, at most 9 levels (153M entries)
+  // about eight cells per leaf at the deepest table level (a wave's box then spans mostly
+  // leaves there), at most 9 levels (153M entries, 0.6 GB)
   int l = 1;
-  while (l < 9 && ((int64_t)1 << (3 * l)) < n_leaves) l++;
+  while (l < 9 && ((int64_t)1 << (3 * l)) < 8 * n_leaves) l++;
   if (l > max_inner_depth + 1) l = max_inner_depth + 1;
   return l < 0 ? 0 : l;
 }

@@ -1,7 +1,8 @@
 """Per-rank cost of one ICP iteration at world size W, probed on one GPU (no collectives): the
 full 10M target, rank 0's source shard (spatial: a kd-order range; SPATIAL=0: a plain range of the
-shuffled cloud). Estimates the strong-scaling floor of bench.py --gpus W
-(the real run adds two RCCL all-gathers of one record per iteration)."""
+shuffled cloud). Estimates the strong-scaling floor of bench.py --gpus W. RCCL=1 runs the
+iterations over a 1-rank RCCL communicator: the multi-rank path (two ncclAllGather + rank-order
+device merges per iteration) without the network."""
 import json
 import os
 import sys
@@ -18,6 +19,8 @@ worlds = [int(w) for w in (sys.argv[1] if len(sys.argv) > 1 else "1,2,4,8").spli
 tgt, src, _ = icp.synth_pair(n)
 ctx = icp.Context(0)
 ctx.set_target(tgt, 10, 20, icp.RULES_ENGINE)
+if os.environ.get("RCCL", "0") == "1":
+    ctx.comm_init(1, 0, icp.Context.unique_id())
 order = icp.source_shard_order(src) if os.environ.get("SPATIAL", "1") == "1" else np.arange(n)
 for w in worlds:
     lo, hi = shard_range(n, 0, w)
@@ -32,7 +35,7 @@ for w in worlds:
     ctx.synchronize()
     dt = (time.perf_counter() - t0) / k
     nn, it = ctx.timings(k)
-    print(json.dumps({"world": w, "shard": hi - lo, "ms_per_step": round(dt * 1e3, 4),
+    print(json.dumps({"world": w, "rccl": os.environ.get("RCCL", "0") == "1", "shard": hi - lo, "ms_per_step": round(dt * 1e3, 4),
                       "knn_ms": round(float(np.mean(nn)), 4), "iter_device_ms": round(float(np.mean(it)), 4),
                       "est_mcorr_s": round(n / dt / 1e6, 1)}), flush=True)
     sess.finish()
