@@ -608,14 +608,25 @@ __device__ __forceinline__ int cell_starts(const NNLaunch& a, double blx, double
   return count;
 }
 
+// A node record loaded whole: four 16-B loads of one 64-B line, all in flight together.
+struct NodeLoad {
+  double2 l01, l2h0, h12;
+  int4 topo;  // first, meta, depth, pad
+};
+__device__ __forceinline__ NodeLoad load_node(const NodeRec* rr) {
+  NodeLoad n;
+  n.l01 = *reinterpret_cast<const double2*>(&rr->lo[0]);
+  n.l2h0 = *reinterpret_cast<const double2*>(&rr->lo[2]);
+  n.h12 = *reinterpret_cast<const double2*>(&rr->hi[1]);
+  n.topo = *reinterpret_cast<const int4*>(&rr->first);
+  return n;
+}
+
 // Children of an inner node that meet the closed box [bl, bh] (child o spans [lo or mid,
 // mid or hi] per axis, octree.cpp:115-120), as a bit mask over octants.
-__device__ __forceinline__ uint32_t children_in_box(const NodeRec* rr, uint32_t mask, double blx, double bly,
+__device__ __forceinline__ uint32_t children_in_box(const NodeLoad& n, uint32_t mask, double blx, double bly,
                                                     double blz, double bhx, double bhy, double bhz) {
-  const double2 l01 = *reinterpret_cast<const double2*>(&rr->lo[0]);
-  const double2 l2h0 = *reinterpret_cast<const double2*>(&rr->lo[2]);
-  const double2 h12 = *reinterpret_cast<const double2*>(&rr->hi[1]);
-  const double lx = l01.x, ly = l01.y, lz = l2h0.x, hx = l2h0.y, hy = h12.x, hz = h12.y;
+  const double lx = n.l01.x, ly = n.l01.y, lz = n.l2h0.x, hx = n.l2h0.y, hy = n.h12.x, hz = n.h12.y;
   const double mx = (lx + hx) / 2, my = (ly + hy) / 2, mz = (lz + hz) / 2;
   const bool x0 = lx <= bhx && mx >= blx, x1 = mx <= bhx && hx >= blx;
   const bool y0 = ly <= bhy && my >= bly, y1 = my <= bhy && hy >= bly;

@@ -284,11 +284,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
       // only child meeting B while there is exactly one.
       int32_t start = 0;
       while (true) {
-        const NodeRec* rr = a.nodes + start;
-        const int2 topo = *reinterpret_cast<const int2*>(&rr->first);
+        const NodeLoad nd = load_node(a.nodes + start);
+        const int2 topo = make_int2(nd.topo.x, nd.topo.y);
         const uint32_t meta = (uint32_t)topo.y;
         if (meta & kLeafBit) break;
-        uint32_t kids = children_in_box(rr, meta & 0xffu, blx, bly, blz, bhx, bhy, bhz);
+        uint32_t kids = children_in_box(nd, meta & 0xffu, blx, bly, blz, bhx, bhy, bhz);
         kids = (uint32_t)__builtin_amdgcn_readfirstlane((int)kids);
         if (__builtin_popcount(kids) != 1) break;
         const uint32_t o = (uint32_t)__builtin_ctz(kids);
@@ -297,33 +297,42 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
       }
       if (lane == 0) queue[0] = start;
     }
-    // Every batch pops up to 64 nodes, which already meet B (tested by their parent; the start
-    // nodes by the cell box or the descent), appends the points of its leaves to the candidate
-    // list and pushes its children meeting B. Most recent first: the live set stays small.
+    // Every batch pops up to 128 nodes (two per lane, both loads in flight), which already meet
+    // B (tested by their parent; the start nodes by the cell box or the descent), appends the
+    // points of its leaves to the candidate list and pushes its children meeting B. Most recent
+    // first: the live set stays small.
     wave_lds_fence();
     while (tail > 0) {
-      const int batch = tail < 64 ? tail : 64;
-      const bool has = lane < batch;
-      bool leaf = false;
-      int32_t first = 0;
-      uint32_t meta = 0, kids = 0;
-      if (has) {
-        const NodeRec* rr = a.nodes + queue[tail - batch + lane];
-        const int2 topo = *reinterpret_cast<const int2*>(&rr->first);
-        first = topo.x;
-        meta = (uint32_t)topo.y;
-        leaf = (meta & kLeafBit) != 0;
-        if (!leaf) kids = children_in_box(rr, meta & 0xffu, blx, bly, blz, bhx, bhy, bhz);
+      const int batch = tail < 128 ? tail : 128;
+      const int e0 = tail - batch + lane;
+      const bool has0 = lane < batch, has1 = lane + 64 < batch;
+      int32_t first0 = 0, first1 = 0;
+      uint32_t meta0 = 0, meta1 = 0, kids0 = 0, kids1 = 0;
+      // both records whole (box and topology) in one round trip; lanes without a node read the
+      // root (in bounds, ignored)
+      const NodeLoad nd0 = load_node(a.nodes + (has0 ? queue[e0] : 0));
+      const NodeLoad nd1 = load_node(a.nodes + (has1 ? queue[e0 + 64] : 0));
+      if (has0) {
+        first0 = nd0.topo.x;
+        meta0 = (uint32_t)nd0.topo.y;
       }
+      if (has1) {
+        first1 = nd1.topo.x;
+        meta1 = (uint32_t)nd1.topo.y;
+      }
+      if (has0 && !(meta0 & kLeafBit)) kids0 = children_in_box(nd0, meta0 & 0xffu, blx, bly, blz, bhx, bhy, bhz);
+      if (has1 && !(meta1 & kLeafBit)) kids1 = children_in_box(nd1, meta1 & 0xffu, blx, bly, blz, bhx, bhy, bhz);
       // a leaf contributes its points (contiguous in leaf order) to the candidate list
-      const int lcnt = (has && leaf) ? (int)(meta & ~kLeafBit) : 0;
+      const int lc0 = (has0 && (meta0 & kLeafBit)) ? (int)(meta0 & ~kLeafBit) : 0;
+      const int lc1 = (has1 && (meta1 & kLeafBit)) ? (int)(meta1 & ~kLeafBit) : 0;
+      const int lcnt = lc0 + lc1;
       int ltot;
       const int lincl = wave_incl_scan(lcnt, &ltot);
       const int lpos = nleaf + lincl - lcnt;
       if (lcnt > 0 && lpos + lcnt <= kWavePoints)
-        for (int c = 0; c < lcnt; c++) plist[lpos + c] = first + c;
+        for (int c = 0; c < lcnt; c++) plist[lpos + c] = c < lc0 ? first0 + c : first1 + (c - lc0);
       nleaf += ltot;
-      const int nch = __builtin_popcount(kids);
+      const int n0 = __builtin_popcount(kids0), nch = n0 + __builtin_popcount(kids1);
       int tot;
       const int incl = wave_incl_scan(nch, &tot);
       tail -= batch;  // the popped entries are in registers; children overwrite them
@@ -332,12 +341,17 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
         break;
       }
       int off = tail + incl - nch;
-      const uint32_t mask = meta & 0xffu;
-      uint32_t kk = kids;
+      uint32_t kk = kids0;
       while (kk) {
         const uint32_t o = (uint32_t)__builtin_ctz(kk);
         kk &= kk - 1u;
-        queue[off++] = first + __builtin_popcount(mask & ((1u << o) - 1u));
+        queue[off++] = first0 + __builtin_popcount(meta0 & 0xffu & ((1u << o) - 1u));
+      }
+      kk = kids1;
+      while (kk) {
+        const uint32_t o = (uint32_t)__builtin_ctz(kk);
+        kk &= kk - 1u;
+        queue[off++] = first1 + __builtin_popcount(meta1 & 0xffu & ((1u << o) - 1u));
       }
       tail += tot;
       if (kDbgCounts && a.dbg && lane == 0) atomicAdd(&a.dbg[5], 1ull);
