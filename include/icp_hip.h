@@ -66,7 +66,11 @@ typedef struct icp_hip_config {
   int32_t xcd_blocks;     /* > 0: the wave search's blocks are renumbered so that each XCD (own
                              L2) takes runs of this many consecutive (spatially adjacent)
                              blocks, dealt round-robin over the XCDs; 0: hardware order  dflt 256 */
-  int32_t reserved[6];    /* zero */
+  int32_t scan_groups;    /* 1, 2 or 4: the fp32 filter scan of a wave splits its lanes into this
+                             many kd sub-buckets, each scanning only the candidates inside its
+                             own box (fewer distance evaluations per query, more staging
+                             work: measured neutral at 2, slower at 4 on config 4)        dflt 1 */
+  int32_t reserved[5];    /* zero */
 } icp_hip_config;
 
 /* Slots of icp_hip_debug_counters (summed over the last iterate's search launches). */

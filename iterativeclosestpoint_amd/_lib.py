@@ -58,7 +58,7 @@ class HipConfig(C.Structure):
     _fields_ = [
         ("search", C.c_int32), ("scan32", C.c_int32), ("cell_starts", C.c_int32),
         ("octree_builder", C.c_int32), ("join_factor", C.c_double), ("debug_counters", C.c_int32),
-        ("xcd_blocks", C.c_int32), ("reserved", C.c_int32 * 6),
+        ("xcd_blocks", C.c_int32), ("scan_groups", C.c_int32), ("reserved", C.c_int32 * 5),
     ]
 
 

@@ -109,6 +109,7 @@ static NNLaunch base_launch(const icp_hip_ctx* c) {
   a.join_factor = c->cfg.join_factor;
   a.neg_inf = -__builtin_inff();
   a.xcd_blocks = c->cfg.xcd_blocks;
+  a.scan_groups = c->cfg.scan_groups;
   a.dbg = c->dbg;
   for (int k = 0; k < 3; k++) {
     a.root_lo[k] = c->root_box[k];
@@ -134,6 +135,7 @@ void icp_hip_config_default(icp_hip_config* cfg) {
   cfg->join_factor = 3.0;
   cfg->debug_counters = 0;
   cfg->xcd_blocks = 256;
+  cfg->scan_groups = 1;
 }
 
 int icp_hip_create(icp_hip_ctx** out, int device) { return icp_hip_create_ex(out, device, nullptr); }
@@ -148,6 +150,8 @@ int icp_hip_create_ex(icp_hip_ctx** out, int device, const icp_hip_config* cfg) 
     return fail(ICP_HIP_EINVAL, "config: unknown search");
   if (conf.octree_builder != ICP_BUILD_AUTO && conf.octree_builder != ICP_BUILD_HOST)
     return fail(ICP_HIP_EINVAL, "config: unknown octree builder");
+  if (conf.scan_groups != 1 && conf.scan_groups != 2 && conf.scan_groups != 4)
+    return fail(ICP_HIP_EINVAL, "config: scan_groups must be 1, 2 or 4");
   if (conf.xcd_blocks < 0 || conf.xcd_blocks > (1 << 20)) return fail(ICP_HIP_EINVAL, "config: xcd_blocks out of [0, 2^20]");
   if (!(conf.join_factor >= 1.0 && conf.join_factor <= 1e6))
     return fail(ICP_HIP_EINVAL, "config: join_factor out of [1, 1e6]");

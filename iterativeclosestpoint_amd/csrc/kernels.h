@@ -56,6 +56,7 @@ struct NNLaunch {
   double join_factor;       // a lane joins the wave box if its radius <= this x the mean radius
   float neg_inf;            // -inf (a launch value: an operand the compiler cannot fold)
   int xcd_blocks;           // renumber the wave search's blocks XCD-contiguously
+  int scan_groups;          // lane groups of the fp32 filter scan (1, 2, 4)
 };
 
 // Threads per block of the per-thread search kernels for a given stack depth.

@@ -111,6 +111,35 @@ __device__ __forceinline__ int wave_max_i(int v) {
   v = max(v, __builtin_amdgcn_update_dpp(I, v, 0x143, 0xc, 0xf, false));
   return __builtin_amdgcn_readlane(v, 63);
 }
+// Steps of the same reductions, exposed so that the row (16-lane) and half (32-lane) partial
+// results can be read on the way: after rows_* lane 16 r + 15 holds row r's result, after
+// halves_* lanes 31 and 63 hold the halves', after wave_* lane 63 the wave's.
+__device__ __forceinline__ int rows_min_i(int v) {
+  constexpr int I = 0x7fffffff;
+  v = min(v, __builtin_amdgcn_update_dpp(I, v, 0x111, 0xf, 0xf, false));
+  v = min(v, __builtin_amdgcn_update_dpp(I, v, 0x112, 0xf, 0xf, false));
+  v = min(v, __builtin_amdgcn_update_dpp(I, v, 0x114, 0xf, 0xf, false));
+  return min(v, __builtin_amdgcn_update_dpp(I, v, 0x118, 0xf, 0xf, false));
+}
+__device__ __forceinline__ int rows_max_i(int v) {
+  constexpr int I = (int)0x80000000;
+  v = max(v, __builtin_amdgcn_update_dpp(I, v, 0x111, 0xf, 0xf, false));
+  v = max(v, __builtin_amdgcn_update_dpp(I, v, 0x112, 0xf, 0xf, false));
+  v = max(v, __builtin_amdgcn_update_dpp(I, v, 0x114, 0xf, 0xf, false));
+  return max(v, __builtin_amdgcn_update_dpp(I, v, 0x118, 0xf, 0xf, false));
+}
+__device__ __forceinline__ int halves_min_i(int v) {
+  return min(v, __builtin_amdgcn_update_dpp(0x7fffffff, v, 0x142, 0xa, 0xf, false));
+}
+__device__ __forceinline__ int halves_max_i(int v) {
+  return max(v, __builtin_amdgcn_update_dpp((int)0x80000000, v, 0x142, 0xa, 0xf, false));
+}
+__device__ __forceinline__ int wave_min_from_halves(int v) {
+  return min(v, __builtin_amdgcn_update_dpp(0x7fffffff, v, 0x143, 0xc, 0xf, false));
+}
+__device__ __forceinline__ int wave_max_from_halves(int v) {
+  return max(v, __builtin_amdgcn_update_dpp((int)0x80000000, v, 0x143, 0xc, 0xf, false));
+}
 __device__ __forceinline__ float wave_sum_f(float v) {
   v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x111, 0xf, 0xf, true));
   v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x112, 0xf, 0xf, true));

@@ -164,8 +164,9 @@ __device__ __forceinline__ unsigned xcd_block(unsigned chunk) {
   return ((k / chunk) * 8u + x) * chunk + k % chunk;
 }
 
-template <bool APPLY>
+template <bool APPLY, int NG>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) k_nn_wave(NNLaunch a) {
+  static_assert(NG == 1 || NG == 2 || NG == 4, "scan groups: 1, 2 or 4");
   extern __shared__ __attribute__((aligned(16))) unsigned long long lds_raw[];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int32_t i = (int32_t)(xcd_block((unsigned)a.xcd_blocks) * blockDim.x + threadIdx.x);  // n <= INT32_MAX
@@ -246,27 +247,65 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
   // the join rule is a heuristic (any subset may join): fp32 mean
   const float mean_r = wave_sum_f(r) * __builtin_amdgcn_rcpf((float)(cmask ? __popcll(cmask) : 1));
   bool join = cand && r <= (float)a.join_factor * mean_r;
+  // The scan groups (NG kd sub-buckets of 64 / NG lanes) get their own boxes, over their own
+  // joined lanes, from the same reductions (row / half partial results on the way).
   double blx = 0.0, bly = 0.0, blz = 0.0, bhx = -1.0, bhy = -1.0, bhz = -1.0;
+  double ox_ = 0.0, oy_ = 0.0, oz_ = 0.0;
+  float glo[NG][3], ghi[NG][3];  // group boxes relative to o (wave-uniform); empty: +inf / -inf
   {
     const unsigned long long jm = __ballot(join);
     if (jm != 0) {
       const int ol = __builtin_ctzll(jm);
-      const double ox_ = readlane_d(qx, ol), oy_ = readlane_d(qy, ol), oz_ = readlane_d(qz, ol);
-      float lo[3], hi[3];
+      ox_ = readlane_d(qx, ol);
+      oy_ = readlane_d(qy, ol);
+      oz_ = readlane_d(qz, ol);
       const double dq[3] = {qx - ox_, qy - oy_, qz - oz_};
+      float wlo[3], whi[3];
 #pragma unroll
       for (int k = 0; k < 3; k++) {
         const float d = (float)dq[k];
         const float m = (__builtin_fabsf(d) + r) * 0x1p-21f + 0x1p-126f;
-        lo[k] = join ? (d - r) - m : __builtin_inff();
-        hi[k] = join ? (d + r) + m : -__builtin_inff();
+        int kl = fkey(join ? (d - r) - m : __builtin_inff());
+        int kh = fkey(join ? (d + r) + m : -__builtin_inff());
+        kl = rows_min_i(kl);
+        kh = rows_max_i(kh);
+        if (NG == 4) {
+#pragma unroll
+          for (int g = 0; g < 4; g++) {
+            glo[g][k] = funkey(__builtin_amdgcn_readlane(kl, 16 * g + 15));
+            ghi[g][k] = funkey(__builtin_amdgcn_readlane(kh, 16 * g + 15));
+          }
+        }
+        kl = halves_min_i(kl);
+        kh = halves_max_i(kh);
+        if (NG == 2) {
+#pragma unroll
+          for (int g = 0; g < 2; g++) {
+            glo[g][k] = funkey(__builtin_amdgcn_readlane(kl, 32 * g + 31));
+            ghi[g][k] = funkey(__builtin_amdgcn_readlane(kh, 32 * g + 31));
+          }
+        }
+        wlo[k] = funkey(__builtin_amdgcn_readlane(wave_min_from_halves(kl), 63));
+        whi[k] = funkey(__builtin_amdgcn_readlane(wave_max_from_halves(kh), 63));
+        if (NG == 1) {
+          glo[0][k] = wlo[k];
+          ghi[0][k] = whi[k];
+        }
       }
-      blx = box_lo(ox_, funkey(wave_min_i(fkey(lo[0]))));
-      bly = box_lo(oy_, funkey(wave_min_i(fkey(lo[1]))));
-      blz = box_lo(oz_, funkey(wave_min_i(fkey(lo[2]))));
-      bhx = box_hi(ox_, funkey(wave_max_i(fkey(hi[0]))));
-      bhy = box_hi(oy_, funkey(wave_max_i(fkey(hi[1]))));
-      bhz = box_hi(oz_, funkey(wave_max_i(fkey(hi[2]))));
+      blx = box_lo(ox_, wlo[0]);
+      bly = box_lo(oy_, wlo[1]);
+      blz = box_lo(oz_, wlo[2]);
+      bhx = box_hi(ox_, whi[0]);
+      bhy = box_hi(oy_, whi[1]);
+      bhz = box_hi(oz_, whi[2]);
+    } else {
+#pragma unroll
+      for (int g = 0; g < NG; g++)
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+          glo[g][k] = __builtin_inff();
+          ghi[g][k] = -__builtin_inff();
+        }
     }
   }
 
@@ -378,12 +417,32 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
                              dmax_(bhz - ocz, ocz - blz)) * (1.0 + 0x1p-40);
     if (ext >= 0x1p-40 && ext <= 0x1p60) {
       const float qx32 = (float)(qx - ocx), qy32 = (float)(qy - ocy), qz32 = (float)(qz - ocz);
-      // staging area: points in pairs, [x0 x1 y0 y1 z0 z1 w0 w1] (32 B), so that one packed fp32
-      // instruction (v_pk_add/mul/fma_f32) evaluates an axis of two points
+      // Group boxes in the scan frame (offsets from B's centre), widened by ext 2^-20: a point
+      // of a joined lane's ball is staged for the lane's group whatever the fp32 rounding of its
+      // offset (<= ext 2^-24). A staged point has |offset| <= ext (1 + 2^-20) (ext_s below).
+      const float mg = (float)(ext * 0x1p-20);
+      const float dox = (float)(ox_ - ocx), doy = (float)(oy_ - ocy), doz = (float)(oz_ - ocz);
+      float gl[NG][3], gh[NG][3];
+      // wave-uniform: kept in scalar registers (readfirstlane), not in 6 NG vector registers
+      auto uni = [](float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); };
+#pragma unroll
+      for (int g = 0; g < NG; g++) {
+        gl[g][0] = uni((glo[g][0] + dox) - mg);
+        gl[g][1] = uni((glo[g][1] + doy) - mg);
+        gl[g][2] = uni((glo[g][2] + doz) - mg);
+        gh[g][0] = uni((ghi[g][0] + dox) + mg);
+        gh[g][1] = uni((ghi[g][1] + doy) + mg);
+        gh[g][2] = uni((ghi[g][2] + doz) + mg);
+      }
+      constexpr int S = 64 / NG;  // lanes of a group = points of a group's segment per round
+      const int gq = lane / S;    // this lane's group
+      // staging area: NG segments of S points, in pairs [x0 x1 y0 y1 z0 z1 w0 w1] (32 B) so that
+      // one packed fp32 instruction (v_pk_add/mul/fma_f32) evaluates an axis of two points; pair
+      // k of group g at (k NG + g): the groups' concurrent reads fall on distinct banks
       float* stage32 = reinterpret_cast<float*>(wl);
       // Selection keys: the fp32 squared distance with its low 6 bits replaced by the point's slot
-      // in the chunk (v_bfi), so that the two smallest are kept by two med3 per point and the
-      // winner is found from its slot once per chunk. A key is within 63 ulps of its value, and
+      // in the segment (v_bfi), so that the two smallest are kept by two med3 per point and the
+      // winner is found from its slot once per round. A key is within 63 ulps of its value, and
       // s2 & ~63 is a lower bound of the second-smallest value; keys are finite and >= 0 (offsets
       // <= ext <= 2^60, pads far but finite), so float order is key order.
       const float ninf = a.neg_inf;  // -inf from the launch record: an opaque med3 operand
@@ -397,31 +456,57 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
         const double2 xy = *reinterpret_cast<const double2*>(&p->x);
         nxtp = make_double4(xy.x, xy.y, p->z, __longlong_as_double((long long)g));
       }
+      typedef float f2 __attribute__((ext_vector_type(2)));
+      typedef int v4i __attribute__((ext_vector_type(4)));
+      const f2 qx2 = {qx32, qx32}, qy2 = {qy32, qy32}, qz2 = {qz32, qz32};
+      auto sel = [&](float sq, uint32_t sl) {
+        const float key = __uint_as_float((sl & 63u) | (__float_as_uint(sq) & ~63u));
+        k2 = __builtin_amdgcn_fmed3f(k1, k2, key);
+        k1 = __builtin_amdgcn_fmed3f(k1, key, ninf);
+      };
+      auto eval2 = [&](const v4i xy, const v4i zw, uint32_t sl) {
+        const f2 X = {__int_as_float(xy.x), __int_as_float(xy.y)};
+        const f2 Y = {__int_as_float(xy.z), __int_as_float(xy.w)};
+        const f2 Z = {__int_as_float(zw.x), __int_as_float(zw.y)};
+        const f2 dx = X - qx2, dy = Y - qy2, dz = Z - qz2;
+        const f2 sq = __builtin_elementwise_fma(dz, dz, __builtin_elementwise_fma(dy, dy, dx * dx));
+        sel(sq.x, sl);
+        sel(sq.y, sl + 1u);
+      };
+      const v4i* st4 = reinterpret_cast<const v4i*>(stage32) + 2 * gq;  // this group's pair 0
       for (int base = 0; base < npts; base += 64) {
-        const bool nin = base + lane < npts && nxtp.x >= blx && nxtp.x <= bhx && nxtp.y >= bly && nxtp.y <= bhy &&
-                         nxtp.z >= blz && nxtp.z <= bhz;
-        const unsigned long long im = __ballot(nin);
-        const int slot = mask_rank(im);
+        const bool valid = base + lane < npts;
         const float vx = (float)(nxtp.x - ocx), vy = (float)(nxtp.y - ocy), vz = (float)(nxtp.z - ocz);
         const float vw = __int_as_float((int)__double_as_longlong(nxtp.w));
-        const int m = __popcll(im);
-        wave_lds_fence();  // previous chunk's reads are done before overwriting the staging slots
-        if (nin) {
-          float* sp = stage32 + 8 * (slot >> 1) + (slot & 1);
-          sp[0] = vx;
-          sp[2] = vy;
-          sp[4] = vz;
-          sp[6] = vw;
-        }
-        if ((m & 1) && lane == 63) {
-          // odd count: the last pair's second point far away (finite: its key never wins and
-          // never becomes the second smallest of a lane that scanned a real point)
-          float* sp = stage32 + 8 * (m >> 1) + 1;
-          sp[0] = 0x1p60f;
-          sp[2] = 0x1p60f;
-          sp[4] = 0x1p60f;
-        }
-        wave_lds_fence();
+        int cn[NG];
+        int maxc = 0;
+        // group membership, rank among the group's points of the chunk, and (first round) the
+        // store into the group's segment; later rounds (more than S points of one group in one
+        // chunk, rare) test again rather than keep NG ranks and masks live
+        auto stage_round = [&](int r0, bool count) {
+#pragma unroll
+          for (int g = 0; g < NG; g++) {
+            const bool in = valid && vx >= gl[g][0] && vx <= gh[g][0] && vy >= gl[g][1] && vy <= gh[g][1] &&
+                            vz >= gl[g][2] && vz <= gh[g][2];
+            const unsigned long long mk = __ballot(in);
+            if (count) {
+              cn[g] = __popcll(mk);
+              maxc = cn[g] > maxc ? cn[g] : maxc;
+            }
+            const int j = mask_rank(mk) - r0;
+            if (in && j >= 0 && j < S) {
+              float* sp = stage32 + 8 * ((j >> 1) * NG + g) + (j & 1);
+              sp[0] = vx;
+              sp[2] = vy;
+              sp[4] = vz;
+              sp[6] = vw;
+            }
+          }
+        };
+        wave_lds_fence();  // the previous round's reads are done before its slots are rewritten
+        stage_round(0, true);
+#pragma unroll
+        for (int g = 0; g < NG; g++) scanned_pts += cn[g];
         const int nb = base + 64;
         if (nb + lane < npts) {
           const int32_t g = plist[nb + lane];
@@ -429,40 +514,39 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
           const double2 xy = *reinterpret_cast<const double2*>(&p->x);
           nxtp = make_double4(xy.x, xy.y, p->z, __longlong_as_double((long long)g));
         }
-        scanned_pts += m;
-        // lockstep over the staged pairs (16-B broadcast reads); one packed instruction evaluates
-        // an axis of two points
-        typedef float f2 __attribute__((ext_vector_type(2)));
-        typedef int v4i __attribute__((ext_vector_type(4)));
-        const f2 qx2 = {qx32, qx32}, qy2 = {qy32, qy32}, qz2 = {qz32, qz32};
-        const float k1_in = k1;
-        auto sel = [&](float sq, uint32_t sl) {
-          const float key = __uint_as_float((sl & 63u) | (__float_as_uint(sq) & ~63u));
-          k2 = __builtin_amdgcn_fmed3f(k1, k2, key);
-          k1 = __builtin_amdgcn_fmed3f(k1, key, ninf);
-        };
-        auto eval2 = [&](const v4i xy, const v4i zw, uint32_t sl) {
-          const f2 X = {__int_as_float(xy.x), __int_as_float(xy.y)};
-          const f2 Y = {__int_as_float(xy.z), __int_as_float(xy.w)};
-          const f2 Z = {__int_as_float(zw.x), __int_as_float(zw.y)};
-          const f2 dx = X - qx2, dy = Y - qy2, dz = Z - qz2;
-          const f2 sq = __builtin_elementwise_fma(dz, dz, __builtin_elementwise_fma(dy, dy, dx * dx));
-          sel(sq.x, sl);
-          sel(sq.y, sl + 1u);
-        };
-        const v4i* st4 = reinterpret_cast<const v4i*>(stage32);
-        const int mp = (m + 1) >> 1;
-        int k = 0;
-        for (; k + 2 <= mp; k += 2) {
-          const v4i a0 = st4[2 * k], b0 = st4[2 * k + 1], a1 = st4[2 * k + 2], b1 = st4[2 * k + 3];
-          eval2(a0, b0, 2u * k);
-          eval2(a1, b1, 2u * k + 2u);
-        }
-        if (k < mp) eval2(st4[2 * k], st4[2 * k + 1], 2u * k);
-        // the winner of this chunk, if it improved the lane's best: its index from its slot
-        if (k1 != k1_in) {
-          const uint32_t sl = __float_as_uint(k1) & 63u;
-          p1 = __float_as_int(stage32[8 * (sl >> 1) + 6 + (sl & 1u)]);
+        for (int r0 = 0; r0 < maxc; r0 += S) {
+          if (r0 > 0) {
+            wave_lds_fence();
+            stage_round(r0, false);
+          }
+          // every segment padded to the round's even length with far points (index -1)
+          int len = maxc - r0 < S ? maxc - r0 : S;
+          len = (len + 1) & ~1;
+          {
+            const int pg = lane / S, pj = lane % S;
+            int c = cn[0];
+#pragma unroll
+            for (int g = 1; g < NG; g++) c = pg == g ? cn[g] : c;
+            c -= r0;
+            if (pj >= c && pj < len) {
+              float* sp = stage32 + 8 * ((pj >> 1) * NG + pg) + (pj & 1);
+              sp[0] = 0x1p62f;
+              sp[2] = 0x1p62f;
+              sp[4] = 0x1p62f;
+              sp[6] = __int_as_float(-1);
+            }
+          }
+          wave_lds_fence();
+          // lockstep over this group's staged pairs (each group's 16-B reads broadcast)
+          const float k1_in = k1;
+          const int mp = len >> 1;
+#pragma unroll 1
+          for (int k = 0; k < mp; k++) eval2(st4[2 * NG * k], st4[2 * NG * k + 1], 2u * k);
+          // the winner of this round, if it improved the lane's best: its index from its slot
+          if (k1 != k1_in) {
+            const uint32_t sl = __float_as_uint(k1) & 63u;
+            p1 = __float_as_int(stage32[8 * ((sl >> 1) * NG + gq) + 6 + (sl & 1u)]);
+          }
         }
       }
       const float s2 = __uint_as_float(__float_as_uint(k2) & ~63u);  // <= the second-smallest value
@@ -473,7 +557,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
         const double dx = p->x - qx, dy = p->y - qy, dz = p->z - qz;
         b64 = dx * dx + dy * dy + dz * dz;
       }
-      const double lb2 = scan32_lower_bound(s2, ext);
+      const double lb2 = scan32_lower_bound(s2, ext * (1.0 + 0x1p-19));
       // Decided lanes: nothing scanned; every point beyond the guess (the fp32 winner and the
       // bound of the rest: the per-lane search takes it, as after an fp64 scan); or a certified
       // winner within the guess. Anything else (a near tie, or a winner beyond u while another
@@ -801,8 +885,15 @@ hipError_t launch_nn(const NNLaunch& a, hipStream_t s) {
   // wave search -> ball search -> per-lane search / exact DFS
   const unsigned wgrid = grid_for(a.n, 256);
   const size_t wshm = (size_t)(256 / 64) * kWaveLds;
-  if (a.apply) hipLaunchKernelGGL((k_nn_wave<true>), dim3(wgrid), dim3(256), wshm, s, a);
-  else hipLaunchKernelGGL((k_nn_wave<false>), dim3(wgrid), dim3(256), wshm, s, a);
+  switch ((a.apply ? 8 : 0) + a.scan_groups) {
+    case 9: hipLaunchKernelGGL((k_nn_wave<true, 1>), dim3(wgrid), dim3(256), wshm, s, a); break;
+    case 10: hipLaunchKernelGGL((k_nn_wave<true, 2>), dim3(wgrid), dim3(256), wshm, s, a); break;
+    case 12: hipLaunchKernelGGL((k_nn_wave<true, 4>), dim3(wgrid), dim3(256), wshm, s, a); break;
+    case 1: hipLaunchKernelGGL((k_nn_wave<false, 1>), dim3(wgrid), dim3(256), wshm, s, a); break;
+    case 2: hipLaunchKernelGGL((k_nn_wave<false, 2>), dim3(wgrid), dim3(256), wshm, s, a); break;
+    case 4: hipLaunchKernelGGL((k_nn_wave<false, 4>), dim3(wgrid), dim3(256), wshm, s, a); break;
+    default: return hipErrorInvalidValue;
+  }
   if (a.ev_fast_done) (void)hipEventRecord(a.ev_fast_done, s);
   // the lists are short (usually empty after the first iteration): small grids of 64-thread
   // blocks, grid-stride over the list

@@ -258,7 +258,9 @@ def test_fallback_share_small_on_scans(icp, gpu_ctx):
                                    (1_000_000, {"cell_starts": 0}),
                                    (300_000, {"cell_starts": 0, "scan32": 0}),
                                    (1_000_000, {"join_factor": 1e6}),
-                                   (300_000, {"octree_builder": 1})])
+                                   (300_000, {"octree_builder": 1}),
+                                   (1_000_000, {"scan_groups": 2}), (1_000_000, {"scan_groups": 4}),
+                                   (300_000, {"xcd_blocks": 0})])
 def test_scan32_matches_fp64_scan(icp, n, cfg):
     """Every configuration of the certified search (fp32 filter scan vs fp64 scan, cell-table
     starts vs root descent, join rule, host-built octree) returns exactly the default's
@@ -284,7 +286,7 @@ def test_scan32_matches_fp64_scan(icp, n, cfg):
         np.testing.assert_array_equal(ia, ib)
         np.testing.assert_array_equal(da, db)
         assert fa == fb
-        if set(cfg) <= {"scan32", "octree_builder"}:  # the same candidate sets
+        if set(cfg) <= {"scan32", "octree_builder", "scan_groups", "xcd_blocks"}:  # the same candidate sets
             assert ba == bb
 
 

@@ -8,16 +8,16 @@ REPO=$(pwd)
 OUT=$REPO/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-BENCH="$REPO/bench.py --points $N --no-cpu-baseline"
+BENCH="$REPO/bench.py --points $N --no-cpu-baseline --no-parity"
 cd /tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o "$TAG" -- \
-  python3 $BENCH --steps 10 --warmup 3 > "$OUT/bench_traced.json" 2> "$OUT/trace.err" || exit $?
+  python3 $BENCH --steps 200 --warmup 5 > "$OUT/bench_traced.json" 2> "$OUT/trace.err" || exit $?
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o "$TAG" -- \
-  python3 $BENCH --steps 3 --warmup 1 > /dev/null 2> "$OUT/pmc_fetch.err" || exit $?
+  python3 $BENCH --steps 50 --warmup 5 > /dev/null 2> "$OUT/pmc_fetch.err" || exit $?
 timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o "$TAG" -- \
-  python3 $BENCH --steps 3 --warmup 1 > /dev/null 2> "$OUT/pmc_write.err" || exit $?
+  python3 $BENCH --steps 50 --warmup 5 > /dev/null 2> "$OUT/pmc_write.err" || exit $?
 timeout -k 10 600 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv -d "$OUT/pmc_l2" -o "$TAG" -- \
-  python3 $BENCH --steps 3 --warmup 1 > /dev/null 2> "$OUT/pmc_l2.err" || exit $?
+  python3 $BENCH --steps 50 --warmup 5 > /dev/null 2> "$OUT/pmc_l2.err" || exit $?
 cd "$REPO"
 python3 tools/pmc_traffic.py "$OUT" "$N" 1 > "$OUT/traffic.json"
 cat "$OUT/traffic.json"
