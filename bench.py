@@ -206,6 +206,9 @@ def main() -> int:
     ap.add_argument("--rccl-self", action="store_true",
                     help="one rank: run the iterations over a 1-rank RCCL communicator (the multi-rank "
                          "path: ncclAllGather + rank-order device merges) instead of the plain path")
+    ap.add_argument("--quantize", type=float, default=0.0,
+                    help="round both clouds to this grid (LAS 1.2 stores int32 x scale: 0.001 emulates "
+                         "config 3's 1 mm grid, with its exact ties and duplicates)")
     ap.add_argument("--config", action="append", default=[], metavar="KEY=VALUE",
                     help="icp_hip_config field for the context (A/B of search options), repeatable")
     ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "traffic_latest.json"),
@@ -231,6 +234,9 @@ def main() -> int:
     n = args.points
     t_setup = time.perf_counter()
     tgt, src, T_true = icp.synth_pair(n)
+    if args.quantize > 0:
+        tgt = np.round(tgt / args.quantize) * args.quantize
+        src = np.round(src / args.quantize) * args.quantize
     lo, hi = shard_range(n, rank, world)
     conf = None
     if args.config:
@@ -336,7 +342,8 @@ def main() -> int:
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (icp_synth_pair: N(0, diag(5,5,1)^2) target seed 42; source = R^T(target - t) "
-                    "+ 1 mm noise, 1% outliers, shuffled, seed 43)",
+                    "+ 1 mm noise, 1% outliers, shuffled, seed 43)"
+                    + (f"; both clouds rounded to a {args.quantize} m grid (LAS-style)" if args.quantize > 0 else ""),
             "config": {
                 "workload": f"{CONFIG_NAMES.get(n, 'custom')}: {n}<->{n} synthetic pair, full ICP iteration "
                             f"(engine rules, octree leaf 10 / depth 20), "
