@@ -190,6 +190,24 @@ def parity_leg(icp, ctx, tgt: np.ndarray, src: np.ndarray, iters: int) -> tuple[
     return parity, allcores
 
 
+class stdout_to_stderr:
+    """RCCL prints a version banner on file descriptor 1 when a communicator is created; the bench
+    contract is ONE JSON line on stdout, so native writes go to stderr while RCCL initialises."""
+
+    def __enter__(self):
+        sys.stdout.flush()
+        self.saved = os.dup(1)
+        os.dup2(2, 1)
+        return self
+
+    def __exit__(self, *exc):
+        sys.stdout.flush()
+        import ctypes
+        ctypes.CDLL(None).fflush(None)  # C stdio buffers too, before fd 1 is restored
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -255,11 +273,14 @@ def main() -> int:
             return torch.stack(out).numpy()
         ctx.comm_init_host(world, rank, exchange)
     elif world > 1:
-        uid = [icp.Context.unique_id() if rank == 0 else None]
+        with stdout_to_stderr():
+            uid = [icp.Context.unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
-        ctx.comm_init(world, rank, uid[0])
+        with stdout_to_stderr():
+            ctx.comm_init(world, rank, uid[0])
     elif args.rccl_self:
-        ctx.comm_init(1, 0, icp.Context.unique_id())
+        with stdout_to_stderr():
+            ctx.comm_init(1, 0, icp.Context.unique_id())
     setup_s = time.perf_counter() - t_setup
     build_on_dev, build_ms = ctx.target_build_info()
 
