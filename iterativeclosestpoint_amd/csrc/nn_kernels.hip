@@ -189,10 +189,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
   // Phase 1: the guess (any value is safe: certification also requires best <= u).
   double u = __builtin_inf();
   if (active && finite_q && a.have_prev) {
-    const double dp = a.dist_out[i];
-    const double ex = qx - ox, ey = qy - oy, ez = qz - oz;
-    const double g = dp + disp_upper(ex * ex + ey * ey + ez * ez);
-    u = (g * g) * (1.0 + 0x1p-30);
+    // the previous match is a candidate: its fl(d2) from the moved query bounds the nearest
+    // point's (usually well below (previous residual + displacement)^2)
+    const TgtPt* pp = a.pts + a.pos_out[i];
+    const double2 pxy = *reinterpret_cast<const double2*>(&pp->x);
+    const double dx = pxy.x - qx, dy = pxy.y - qy, dz = pp->z - qz;
+    u = dx * dx + dy * dy + dz * dz;
   } else if (active && finite_q) {
     const NodeRec* r0 = a.nodes;
     double lx = r0->lo[0], ly = r0->lo[1], lz = r0->lo[2], hx = r0->hi[0], hy = r0->hi[1], hz = r0->hi[2];
