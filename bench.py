@@ -227,6 +227,10 @@ def main() -> int:
     ap.add_argument("--quantize", type=float, default=0.0,
                     help="round both clouds to this grid (LAS 1.2 stores int32 x scale: 0.001 emulates "
                          "config 3's 1 mm grid, with its exact ties and duplicates)")
+    ap.add_argument("--duplicates", type=int, default=1,
+                    help="every target point repeated this many times (an exact tie for every query: the "
+                         "certified search's fp64 rescan gives copies of the winner the lowest slot, "
+                         "as the reference's leaf order does)")
     ap.add_argument("--config", action="append", default=[], metavar="KEY=VALUE",
                     help="icp_hip_config field for the context (A/B of search options), repeatable")
     ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "traffic_latest.json"),
@@ -252,6 +256,8 @@ def main() -> int:
     n = args.points
     t_setup = time.perf_counter()
     tgt, src, T_true = icp.synth_pair(n)
+    if args.duplicates > 1:
+        tgt = np.repeat(tgt[: n // args.duplicates + 1], args.duplicates, axis=0)[:n]
     if args.quantize > 0:
         tgt = np.round(tgt / args.quantize) * args.quantize
         src = np.round(src / args.quantize) * args.quantize
@@ -364,7 +370,8 @@ def main() -> int:
             "dtype": "f64",
             "data": "synthetic (icp_synth_pair: N(0, diag(5,5,1)^2) target seed 42; source = R^T(target - t) "
                     "+ 1 mm noise, 1% outliers, shuffled, seed 43)"
-                    + (f"; both clouds rounded to a {args.quantize} m grid (LAS-style)" if args.quantize > 0 else ""),
+                    + (f"; both clouds rounded to a {args.quantize} m grid (LAS-style)" if args.quantize > 0 else "")
+                    + (f"; every target point repeated {args.duplicates}x" if args.duplicates > 1 else ""),
             "config": {
                 "workload": f"{CONFIG_NAMES.get(n, 'custom')}: {n}<->{n} synthetic pair, full ICP iteration "
                             f"(engine rules, octree leaf 10 / depth 20), "

@@ -101,16 +101,9 @@ constexpr int kWavePoints = 1024;  // candidate points per wave
 constexpr int kWaveLds = kWaveQueue * 4 + kWavePoints * 4;  // 5 KB per wave
 static_assert(kWaveQueue * 4 >= 64 * 16 && kWaveQueue * 4 >= 32 * 32, "staging area aliases the stack");
 
-// Upper bound of sqrt(e2) (a displacement; e2 >= 0) from the fp32 square root: (float) rounds by
-// <= 2^-24, v_sqrt_f32 is within 1 ulp, each fp32 product by <= 2^-24; 2^-60 covers e2 below the
-// fp32 normal range. Overflow gives +inf (the lane then has no usable guess).
-__device__ __forceinline__ double disp_upper(double e2) {
-  const float s = __builtin_sqrtf((float)e2 * (1.0f + 0x1p-21f)) * (1.0f + 0x1p-21f) + 0x1p-60f;
-  return (double)s;
-}
-
 // fp32 radius r >= sqrt(u) (1 + 2^-40) + amax 2^-45 (the ball of the wave search's certificate):
-// the fp32 square root rounded up as in disp_upper, the amax term doubled, 2^-49 absolute for u
+// the fp32 square root rounded up ((float) rounds by <= 2^-24, v_sqrt_f32 is within 1 ulp, each
+// fp32 product by <= 2^-24), the amax term doubled, 2^-49 absolute for u
 // below the fp32 normal range, and the sum's rounding covered by the 2^-21 factors.
 __device__ __forceinline__ float ball_radius32(double u, double amax) {
   const float s = __builtin_sqrtf((float)u * (1.0f + 0x1p-21f)) * (1.0f + 0x1p-21f);
@@ -176,12 +169,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
   double4* stage = reinterpret_cast<double4*>(wl);  // after the walk only
   int32_t* plist = queue + kWaveQueue;               // candidate points
 
-  double qx = 0.0, qy = 0.0, qz = 0.0, ox = 0.0, oy = 0.0, oz = 0.0;
-  if (active) {
-    ox = a.x[i];
-    oy = a.y[i];
-    oz = a.z[i];
-  }
+  double qx = 0.0, qy = 0.0, qz = 0.0;
   load_query<APPLY>(a, i, active, qx, qy, qz);
   const bool finite_q = __builtin_isfinite(qx) && __builtin_isfinite(qy) && __builtin_isfinite(qz);
 
@@ -576,6 +564,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
   if (need64) {
     // Points outside B are farther than r from every joined lane (each ball lies in B), so
     // they can neither be a joined lane's nearest point nor sit in its certificate window.
+    // Exact duplicates of the winner (identical coordinates) are not ties: they share its leaf
+    // (identical points take the same octant at every split), where the reference's strict <
+    // keeps the first in leaf order, i.e. the smallest position; `second` is the smallest fl(d2)
+    // of the points that are not copies of the winner (any other equal distance stays a tie).
     wave_lds_fence();
     double4 nxtp = make_double4(0.0, 0.0, 0.0, 0.0);
     bool nin = false;
@@ -610,10 +602,18 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
           const double4 pt = stage[k];
           const double dx = pt.x - qx, dy = pt.y - qy, dz = pt.z - qz;
           const double d2 = dx * dx + dy * dy + dz * dz;
+          const int32_t pi = (int32_t)__double_as_longlong(pt.w);
+          bool dup = false;
+          if (d2 == best) {  // rare: the winner is read back (no registers held for it)
+            const TgtPt* w = a.pts + bpos;
+            dup = w->x == pt.x && w->y == pt.y && w->z == pt.z;
+          }
           if (d2 < best) {
             second = best;
             best = d2;
-            bpos = (int32_t)__double_as_longlong(pt.w);
+            bpos = pi;
+          } else if (dup) {
+            bpos = pi < bpos ? pi : bpos;  // an exact duplicate of the winner: no tie to break
           } else if (d2 < second) {
             second = d2;
           }

@@ -312,6 +312,24 @@ def test_scan32_ties_and_self_queries(icp, oracle, golden_nn):
         np.testing.assert_array_equal(d, od)
 
 
+def test_wave_repeated_targets(icp, oracle):
+    """Every target point stored 2 or 3 times (bench --duplicates): each query's nearest point has
+    exact copies, which the wave kernel's fp64 rescan resolves to the lowest slot; identical
+    indices and distances to the reference-order search."""
+    tgt, src, _ = icp.synth_pair(60_000, yaw_deg=2.0)
+    for rep in (2, 3):
+        t = np.repeat(tgt[: 60_000 // rep + 1], rep, axis=0)[:60_000]
+        with icp.Context(0) as ctx:
+            ctx.set_target(t, 10, 20, icp.RULES_CLI)
+            ctx.set_source(src)
+            ctx.iterate(None, 0, icp.RULES_CLI, 3.0)
+            ctx.iterate(np.eye(4), 1, icp.RULES_CLI, 3.0)
+            idx, d = ctx.get_correspondences()
+        oidx, od = oracle.OracleTree(t).nn(src, init_best=1e20)
+        np.testing.assert_array_equal(idx, oidx)
+        np.testing.assert_array_equal(d, od)
+
+
 def test_session_step_n_equals_steps(icp):
     """icp_session_step_n (the bench's timed loop) is the same loop as repeated icp_session_step:
     identical transforms bit for bit; it stops at convergence like the step loop."""
