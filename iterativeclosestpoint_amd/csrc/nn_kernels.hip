@@ -449,8 +449,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
       typedef float f2 __attribute__((ext_vector_type(2)));
       typedef int v4i __attribute__((ext_vector_type(4)));
       const f2 qx2 = {qx32, qx32}, qy2 = {qy32, qy32}, qz2 = {qz32, qz32};
+      // ~63 in a vector register: with it (a literal cannot be a VOP3 operand on gfx9) the key is
+      // one v_and_or_b32 instead of v_and_b32 + v_or_b32
+      uint32_t kmask = ~63u;
+      asm volatile("" : "+v"(kmask));
       auto sel = [&](float sq, uint32_t sl) {
-        const float key = __uint_as_float((sl & 63u) | (__float_as_uint(sq) & ~63u));
+        const float key = __uint_as_float((__float_as_uint(sq) & kmask) | sl);
         k2 = __builtin_amdgcn_fmed3f(k1, k2, key);
         k1 = __builtin_amdgcn_fmed3f(k1, key, ninf);
       };
@@ -461,7 +465,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
         const f2 dx = X - qx2, dy = Y - qy2, dz = Z - qz2;
         const f2 sq = __builtin_elementwise_fma(dz, dz, __builtin_elementwise_fma(dy, dy, dx * dx));
         sel(sq.x, sl);
-        sel(sq.y, sl + 1u);
+        sel(sq.y, (uint32_t)__builtin_amdgcn_readfirstlane((int)(sl + 1u)));  // a scalar operand
       };
       const v4i* st4 = reinterpret_cast<const v4i*>(stage32) + 2 * gq;  // this group's pair 0
       for (int base = 0; base < npts; base += 64) {
