@@ -70,7 +70,14 @@ typedef struct icp_hip_config {
                              many kd sub-buckets, each scanning only the candidates inside its
                              own box (fewer distance evaluations per query, more staging
                              work: measured neutral at 2, slower at 4 on config 4)        dflt 1 */
-  int32_t reserved[5];    /* zero */
+  int32_t candidate_cache;  /* 1: each wave of the iterate's search keeps the candidate list of
+                               its search box B enlarged by candidate_margin (1/256 units of B's
+                               largest half-extent per side), and the next iterate reuses it
+                               without walking the octree while its new box lies inside
+                               (an exact containment test: results are unchanged); 0: every
+                               iterate walks                                              dflt 1 */
+  int32_t candidate_margin; /* see candidate_cache, in [0, 1024]                         dflt 8 */
+  int32_t reserved[3];    /* zero */
 } icp_hip_config;
 
 /* Slots of icp_hip_debug_counters (summed over the last iterate's search launches). */
@@ -82,6 +89,12 @@ typedef struct icp_hip_config {
 #define ICP_DBG_WALK_BATCHES 5   /* walk batches (up to 64 nodes each)                          */
 #define ICP_DBG_NO_GUESS 6       /* lanes without a usable guess                               */
 #define ICP_DBG_CANDIDATES 7     /* candidate points collected by the walks                    */
+#define ICP_DBG_FP64_WAVES 8     /* waves re-scanned in fp64 (uncertified after the fp32 scan) */
+#define ICP_DBG_STAGED 9         /* points staged for the fp32 scan                            */
+#define ICP_DBG_SCAN_PAIRS 10    /* point pairs evaluated by the fp32 scan (per wave)          */
+#define ICP_DBG_SCAN_ROUNDS 11   /* fp32 scan rounds                                           */
+#define ICP_DBG_CACHE_HITS 12    /* waves that reused their cached candidate list              */
+#define ICP_DBG_CACHE_STORES 13  /* waves that walked and stored their candidate list          */
 #define ICP_DBG_BALL_OVERFLOW 14 /* ball-search queries whose candidate set overflowed         */
 #define ICP_DBG_BALL_POINTS 15   /* points scanned by the ball search                          */
 #define ICP_DBG_CLK_GUESS 16     /* wave clocks (s_memtime): guess + box                       */

@@ -21,7 +21,9 @@ BUILD_AUTO = 0
 BUILD_HOST = 1
 DBG_SLOTS = 24
 # icp_hip.h ICP_DBG_* slot names
-DBG_NAMES = {0: "waves", 1: "overflow_waves", 2: "not_joined", 3: "not_covered", 4: "rescan_points",
+DBG_NAMES = {0: "waves", 1: "overflow_waves", 2: "not_joined", 3: "not_covered", 4: "scanned_points",
+             8: "fp64_scan_waves", 9: "staged_points", 10: "scan_pairs", 11: "scan_rounds",
+             12: "cache_hits", 13: "cache_stores",
              5: "walk_batches", 6: "no_guess", 7: "candidates", 14: "ball_overflow", 15: "ball_points",
              21: "start_nodes"}
 
@@ -58,7 +60,8 @@ class HipConfig(C.Structure):
     _fields_ = [
         ("search", C.c_int32), ("scan32", C.c_int32), ("cell_starts", C.c_int32),
         ("octree_builder", C.c_int32), ("join_factor", C.c_double), ("debug_counters", C.c_int32),
-        ("xcd_blocks", C.c_int32), ("scan_groups", C.c_int32), ("reserved", C.c_int32 * 5),
+        ("xcd_blocks", C.c_int32), ("scan_groups", C.c_int32), ("candidate_cache", C.c_int32),
+        ("candidate_margin", C.c_int32), ("reserved", C.c_int32 * 3),
     ]
 
 

@@ -76,6 +76,8 @@ static void free_source(icp_hip_ctx* c) {
   dfree(c->dist);
   dfree(c->fb_list);
   dfree(c->fb_u);
+  dfree(c->wc_box);
+  dfree(c->wc_ids);
   dfree(c->mparts);
   dfree(c->cparts);
   c->n_src = 0;
@@ -136,6 +138,8 @@ void icp_hip_config_default(icp_hip_config* cfg) {
   cfg->debug_counters = 0;
   cfg->xcd_blocks = 256;
   cfg->scan_groups = 1;
+  cfg->candidate_cache = 1;
+  cfg->candidate_margin = 8;
 }
 
 int icp_hip_create(icp_hip_ctx** out, int device) { return icp_hip_create_ex(out, device, nullptr); }
@@ -153,6 +157,9 @@ int icp_hip_create_ex(icp_hip_ctx** out, int device, const icp_hip_config* cfg) 
   if (conf.scan_groups != 1 && conf.scan_groups != 2 && conf.scan_groups != 4)
     return fail(ICP_HIP_EINVAL, "config: scan_groups must be 1, 2 or 4");
   if (conf.xcd_blocks < 0 || conf.xcd_blocks > (1 << 20)) return fail(ICP_HIP_EINVAL, "config: xcd_blocks out of [0, 2^20]");
+  if (conf.candidate_cache != 0 && conf.candidate_cache != 1) return fail(ICP_HIP_EINVAL, "config: candidate_cache must be 0 or 1");
+  if (conf.candidate_margin < 0 || conf.candidate_margin > 1024)
+    return fail(ICP_HIP_EINVAL, "config: candidate_margin out of [0, 1024]");
   if (!(conf.join_factor >= 1.0 && conf.join_factor <= 1e6))
     return fail(ICP_HIP_EINVAL, "config: join_factor out of [1, 1e6]");
   int ndev = 0;
@@ -355,6 +362,7 @@ int icp_hip_set_target(icp_hip_ctx* c, const double* xyz, int64_t n, int max_poi
   c->n_tgt = n;
   c->init_best = (rules == ICP_RULES_CLI) ? 1e20 : DBL_MAX;  // icp_registration.cpp:201 / octree.cpp:180
   c->have_prev = false;
+  c->wc_gen++;  // cached candidate lists name points of the previous tree
   c->have_results = false;
   return ICP_HIP_OK;
 }
@@ -415,6 +423,13 @@ int icp_hip_set_source(icp_hip_ctx* c, const double* xyz, int64_t n) {
   HIP_TRY(dalloc(&c->dist, n));
   HIP_TRY(dalloc(&c->fb_list, 3 * (size_t)n));
   HIP_TRY(dalloc(&c->fb_u, (size_t)n));
+  if (c->cfg.candidate_cache && n > 0) {
+    const size_t nw = (size_t)((n + 63) / 64);
+    HIP_TRY(dalloc(&c->wc_box, nw));
+    HIP_TRY(dalloc(&c->wc_ids, nw * icp::kWaveCandCap));
+    HIP_TRY(hipMemsetAsync(c->wc_box, 0, nw * sizeof(icp::WaveBox), c->stream));  // generation 0: invalid
+  }
+  c->wc_gen++;
   HIP_TRY(dalloc(&c->mparts, (size_t)(c->nb_mom + merge_scratch_entries(c->nb_mom))));
   HIP_TRY(dalloc(&c->cparts, (size_t)(c->nb_cull + merge_scratch_entries(c->nb_cull))));
   if (n == 0) return ICP_HIP_OK;
@@ -466,6 +481,10 @@ int icp_hip_iterate(icp_hip_ctx* c, const double* T_apply, int iter, int rules, 
   a.fb_u2 = c->fb_u;
   a.fb_count = c->fb_count;
   a.have_prev = c->have_prev ? 1 : 0;
+  a.wc_box = c->wc_box;
+  a.wc_ids = c->wc_ids;
+  a.wc_gen = c->wc_gen;
+  a.wc_margin = c->cfg.candidate_margin / 256.0;
   if (!c->lists_zero) HIP_TRY(hipMemsetAsync(c->fb_count, 0, 3 * sizeof(unsigned int), s));
   c->lists_zero = false;
   if (c->dbg) HIP_TRY(hipMemsetAsync(c->dbg, 0, ICP_DBG_SLOTS * sizeof(unsigned long long), s));

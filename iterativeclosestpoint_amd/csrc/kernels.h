@@ -23,6 +23,16 @@ struct IterDev {
   double pad[4];
 };
 
+// The wave search's candidate cache (one record per wave of 64 queries): the box whose leaves'
+// points were collected, their count and the generation (target / source upload) it belongs to.
+constexpr int kWaveCandCap = 1008;  // candidate points per wave (the list in LDS; ids in the cache)
+struct WaveBox {
+  double lo[3];
+  double hi[3];
+  int32_t count;
+  uint32_t gen;
+};
+
 struct NNLaunch {
   const NodeRec* nodes;
   const TgtPt* pts;
@@ -57,6 +67,10 @@ struct NNLaunch {
   float neg_inf;            // -inf (a launch value: an operand the compiler cannot fold)
   int xcd_blocks;           // renumber the wave search's blocks XCD-contiguously
   int scan_groups;          // lane groups of the fp32 filter scan (1, 2, 4)
+  WaveBox* wc_box;          // candidate cache (iterate only; null: every wave walks)
+  int32_t* wc_ids;          // kWaveCandCap candidate ids per wave
+  uint32_t wc_gen;          // records of this generation are valid
+  double wc_margin;         // a walk collects the leaves of B enlarged by this x B's half-extent
 };
 
 // Threads per block of the per-thread search kernels for a given stack depth.

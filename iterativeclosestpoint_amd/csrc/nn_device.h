@@ -60,6 +60,14 @@ __device__ __forceinline__ double readlane_d(double v, int lane) {
   const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(b >> 32), lane);
   return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
+// A wave-uniform double moved to scalar registers (fp64 arithmetic is vector-only, so uniform
+// results otherwise occupy two vector registers each).
+__device__ __forceinline__ double uniform_d(double v) {
+  const long long b = __double_as_longlong(v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)b);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readfirstlane((int)(b >> 32));
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
 __device__ __forceinline__ double wave_sum_d(double v) {
   v += dpp_d<0x111, 0xf, true>(v);
   v += dpp_d<0x112, 0xf, true>(v);

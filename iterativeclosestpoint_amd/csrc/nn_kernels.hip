@@ -97,7 +97,8 @@ __global__ void __launch_bounds__(256) k_nn_ref(NNLaunch a) {
 // to the exact list.
 constexpr int kWaveQueue = 256;  // node ids of the walk's LIFO stack (staging area after the walk)
 constexpr int kWaveStartK = 2;   // start cells per lane (up to 128 start nodes per wave)
-constexpr int kWavePoints = 1024;  // candidate points per wave
+constexpr int kWavePoints = 1024;  // candidate list area (up to kWaveCandCap ids)
+static_assert(kWaveCandCap <= kWavePoints, "candidate list");
 constexpr int kWaveLds = kWaveQueue * 4 + kWavePoints * 4;  // 5 KB per wave
 static_assert(kWaveQueue * 4 >= 64 * 16 && kWaveQueue * 4 >= 32 * 32, "staging area aliases the stack");
 
@@ -282,12 +283,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
           ghi[0][k] = whi[k];
         }
       }
-      blx = box_lo(ox_, wlo[0]);
-      bly = box_lo(oy_, wlo[1]);
-      blz = box_lo(oz_, wlo[2]);
-      bhx = box_hi(ox_, whi[0]);
-      bhy = box_hi(oy_, whi[1]);
-      bhz = box_hi(oz_, whi[2]);
+      blx = uniform_d(box_lo(ox_, wlo[0]));
+      bly = uniform_d(box_lo(oy_, wlo[1]));
+      blz = uniform_d(box_lo(oz_, wlo[2]));
+      bhx = uniform_d(box_hi(ox_, whi[0]));
+      bhy = uniform_d(box_hi(oy_, whi[1]));
+      bhz = uniform_d(box_hi(oz_, whi[2]));
     } else {
 #pragma unroll
       for (int g = 0; g < NG; g++)
@@ -300,91 +301,135 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
   }
 
   PCLK(t_p2);
-  // Phase 3: the leaves meeting B.
+  // Phase 3: the leaves meeting B. With the candidate cache (iterate only), a walk collects the
+  // leaves meeting B+ = B enlarged by wc_margin x its largest half-extent per side and stores their
+  // points' ids with B+; the next iterate's wave reuses them without walking while its own B lies
+  // inside B+ (every leaf meeting B then meets B+). Staging filters by B, so the larger list
+  // changes nothing but the staging work.
   int nleaf = 0;
   bool overflow = false;
-  if (__ballot(join) != 0) {
-    int tail = 1;
-    if (a.cells) {
-      tail = cell_starts<64, kWaveStartK>(a, blx, bly, blz, bhx, bhy, bhz, lane, 0, queue);
-      if (kDbgCounts && a.dbg && lane == 0) atomicAdd(&a.dbg[21], (unsigned long long)tail);
-    } else {
-      // Wave-uniform descent to the deepest node that holds every leaf meeting B: follow the
-      // only child meeting B while there is exactly one.
-      int32_t start = 0;
-      while (true) {
-        const NodeLoad nd = load_node(a.nodes + start);
-        const int2 topo = make_int2(nd.topo.x, nd.topo.y);
-        const uint32_t meta = (uint32_t)topo.y;
-        if (meta & kLeafBit) break;
-        uint32_t kids = children_in_box(nd, meta & 0xffu, blx, bly, blz, bhx, bhy, bhz);
-        kids = (uint32_t)__builtin_amdgcn_readfirstlane((int)kids);
-        if (__builtin_popcount(kids) != 1) break;
-        const uint32_t o = (uint32_t)__builtin_ctz(kids);
-        start = __builtin_amdgcn_readfirstlane(topo.x + __builtin_popcount((meta & 0xffu) & ((1u << o) - 1u)));
-        if (kDbgCounts && a.dbg && lane == 0) atomicAdd(&a.dbg[21], 1ull);
+  // the cooperative walk over the leaves meeting the box [wl, wh] (wave-uniform)
+  auto walk = [&](double wlx, double wly, double wlz, double whx, double why, double whz) {
+    nleaf = 0;
+    overflow = false;
+      int tail = 1;
+      if (a.cells) {
+        tail = cell_starts<64, kWaveStartK>(a, wlx, wly, wlz, whx, why, whz, lane, 0, queue);
+        if (kDbgCounts && a.dbg && lane == 0) atomicAdd(&a.dbg[21], (unsigned long long)tail);
+      } else {
+        // Wave-uniform descent to the deepest node that holds every leaf meeting B: follow the
+        // only child meeting B while there is exactly one.
+        int32_t start = 0;
+        while (true) {
+          const NodeLoad nd = load_node(a.nodes + start);
+          const int2 topo = make_int2(nd.topo.x, nd.topo.y);
+          const uint32_t meta = (uint32_t)topo.y;
+          if (meta & kLeafBit) break;
+          uint32_t kids = children_in_box(nd, meta & 0xffu, wlx, wly, wlz, whx, why, whz);
+          kids = (uint32_t)__builtin_amdgcn_readfirstlane((int)kids);
+          if (__builtin_popcount(kids) != 1) break;
+          const uint32_t o = (uint32_t)__builtin_ctz(kids);
+          start = __builtin_amdgcn_readfirstlane(topo.x + __builtin_popcount((meta & 0xffu) & ((1u << o) - 1u)));
+          if (kDbgCounts && a.dbg && lane == 0) atomicAdd(&a.dbg[21], 1ull);
+        }
+        if (lane == 0) queue[0] = start;
       }
-      if (lane == 0) queue[0] = start;
-    }
-    // Every batch pops up to 128 nodes (two per lane, both loads in flight), which already meet
-    // B (tested by their parent; the start nodes by the cell box or the descent), appends the
-    // points of its leaves to the candidate list and pushes its children meeting B. Most recent
-    // first: the live set stays small.
-    wave_lds_fence();
-    while (tail > 0) {
-      const int batch = tail < 128 ? tail : 128;
-      const int e0 = tail - batch + lane;
-      const bool has0 = lane < batch, has1 = lane + 64 < batch;
-      int32_t first0 = 0, first1 = 0;
-      uint32_t meta0 = 0, meta1 = 0, kids0 = 0, kids1 = 0;
-      // both records whole (box and topology) in one round trip; lanes without a node read the
-      // root (in bounds, ignored)
-      const NodeLoad nd0 = load_node(a.nodes + (has0 ? queue[e0] : 0));
-      const NodeLoad nd1 = load_node(a.nodes + (has1 ? queue[e0 + 64] : 0));
-      if (has0) {
-        first0 = nd0.topo.x;
-        meta0 = (uint32_t)nd0.topo.y;
-      }
-      if (has1) {
-        first1 = nd1.topo.x;
-        meta1 = (uint32_t)nd1.topo.y;
-      }
-      if (has0 && !(meta0 & kLeafBit)) kids0 = children_in_box(nd0, meta0 & 0xffu, blx, bly, blz, bhx, bhy, bhz);
-      if (has1 && !(meta1 & kLeafBit)) kids1 = children_in_box(nd1, meta1 & 0xffu, blx, bly, blz, bhx, bhy, bhz);
-      // a leaf contributes its points (contiguous in leaf order) to the candidate list
-      const int lc0 = (has0 && (meta0 & kLeafBit)) ? (int)(meta0 & ~kLeafBit) : 0;
-      const int lc1 = (has1 && (meta1 & kLeafBit)) ? (int)(meta1 & ~kLeafBit) : 0;
-      const int lcnt = lc0 + lc1;
-      int ltot;
-      const int lincl = wave_incl_scan(lcnt, &ltot);
-      const int lpos = nleaf + lincl - lcnt;
-      if (lcnt > 0 && lpos + lcnt <= kWavePoints)
-        for (int c = 0; c < lcnt; c++) plist[lpos + c] = c < lc0 ? first0 + c : first1 + (c - lc0);
-      nleaf += ltot;
-      const int n0 = __builtin_popcount(kids0), nch = n0 + __builtin_popcount(kids1);
-      int tot;
-      const int incl = wave_incl_scan(nch, &tot);
-      tail -= batch;  // the popped entries are in registers; children overwrite them
-      if (nleaf > kWavePoints || tail + tot > kWaveQueue) {
-        overflow = true;
-        break;
-      }
-      int off = tail + incl - nch;
-      uint32_t kk = kids0;
-      while (kk) {
-        const uint32_t o = (uint32_t)__builtin_ctz(kk);
-        kk &= kk - 1u;
-        queue[off++] = first0 + __builtin_popcount(meta0 & 0xffu & ((1u << o) - 1u));
-      }
-      kk = kids1;
-      while (kk) {
-        const uint32_t o = (uint32_t)__builtin_ctz(kk);
-        kk &= kk - 1u;
-        queue[off++] = first1 + __builtin_popcount(meta1 & 0xffu & ((1u << o) - 1u));
-      }
-      tail += tot;
-      if (kDbgCounts && a.dbg && lane == 0) atomicAdd(&a.dbg[5], 1ull);
+      // Every batch pops up to 128 nodes (two per lane, both loads in flight), which already meet
+      // B (tested by their parent; the start nodes by the cell box or the descent), appends the
+      // points of its leaves to the candidate list and pushes its children meeting B. Most recent
+      // first: the live set stays small.
       wave_lds_fence();
+      while (tail > 0) {
+        const int batch = tail < 128 ? tail : 128;
+        const int e0 = tail - batch + lane;
+        const bool has0 = lane < batch, has1 = lane + 64 < batch;
+        int32_t first0 = 0, first1 = 0;
+        uint32_t meta0 = 0, meta1 = 0, kids0 = 0, kids1 = 0;
+        // both records whole (box and topology) in one round trip; lanes without a node read the
+        // root (in bounds, ignored)
+        const NodeLoad nd0 = load_node(a.nodes + (has0 ? queue[e0] : 0));
+        const NodeLoad nd1 = load_node(a.nodes + (has1 ? queue[e0 + 64] : 0));
+        if (has0) {
+          first0 = nd0.topo.x;
+          meta0 = (uint32_t)nd0.topo.y;
+        }
+        if (has1) {
+          first1 = nd1.topo.x;
+          meta1 = (uint32_t)nd1.topo.y;
+        }
+        if (has0 && !(meta0 & kLeafBit)) kids0 = children_in_box(nd0, meta0 & 0xffu, wlx, wly, wlz, whx, why, whz);
+        if (has1 && !(meta1 & kLeafBit)) kids1 = children_in_box(nd1, meta1 & 0xffu, wlx, wly, wlz, whx, why, whz);
+        // a leaf contributes its points (contiguous in leaf order) to the candidate list
+        const int lc0 = (has0 && (meta0 & kLeafBit)) ? (int)(meta0 & ~kLeafBit) : 0;
+        const int lc1 = (has1 && (meta1 & kLeafBit)) ? (int)(meta1 & ~kLeafBit) : 0;
+        const int lcnt = lc0 + lc1;
+        int ltot;
+        const int lincl = wave_incl_scan(lcnt, &ltot);
+        const int lpos = nleaf + lincl - lcnt;
+        if (lcnt > 0 && lpos + lcnt <= kWaveCandCap)
+          for (int c = 0; c < lcnt; c++) plist[lpos + c] = c < lc0 ? first0 + c : first1 + (c - lc0);
+        nleaf += ltot;
+        const int n0 = __builtin_popcount(kids0), nch = n0 + __builtin_popcount(kids1);
+        int tot;
+        const int incl = wave_incl_scan(nch, &tot);
+        tail -= batch;  // the popped entries are in registers; children overwrite them
+        if (nleaf > kWaveCandCap || tail + tot > kWaveQueue) {
+          overflow = true;
+          return;
+        }
+        int off = tail + incl - nch;
+        uint32_t kk = kids0;
+        while (kk) {
+          const uint32_t o = (uint32_t)__builtin_ctz(kk);
+          kk &= kk - 1u;
+          queue[off++] = first0 + __builtin_popcount(meta0 & 0xffu & ((1u << o) - 1u));
+        }
+        kk = kids1;
+        while (kk) {
+          const uint32_t o = (uint32_t)__builtin_ctz(kk);
+          kk &= kk - 1u;
+          queue[off++] = first1 + __builtin_popcount(meta1 & 0xffu & ((1u << o) - 1u));
+        }
+        tail += tot;
+        if (kDbgCounts && a.dbg && lane == 0) atomicAdd(&a.dbg[5], 1ull);
+        wave_lds_fence();
+      }
+  };
+  if (__ballot(join) != 0) {
+    const uint32_t wid = (uint32_t)__builtin_amdgcn_readfirstlane((int)i) >> 6;
+    WaveBox* wb = a.wc_box ? a.wc_box + wid : nullptr;
+    bool reuse = false;
+    if (wb)
+      reuse = wb->gen == a.wc_gen && blx >= wb->lo[0] && bly >= wb->lo[1] && blz >= wb->lo[2] && bhx <= wb->hi[0] &&
+              bhy <= wb->hi[1] && bhz <= wb->hi[2];
+    if (reuse) {
+      nleaf = wb->count;
+      const int32_t* ids = a.wc_ids + (size_t)wid * kWaveCandCap;
+      for (int k = lane; k < nleaf; k += 64) plist[k] = ids[k];
+      if (kDbgCounts && a.dbg && lane == 0) atomicAdd(&a.dbg[12], 1ull);
+    } else {
+      // B+ (B itself without the cache); an overflowing B+ makes an overflowing wave (its lanes
+      // take the ball search; ~0.06 % of the waves at 10M with the default margin). Wave-uniform
+      // doubles are kept in scalar registers.
+      const double m = wb ? a.wc_margin * 0.5 * dmax_(dmax_(bhx - blx, bhy - bly), bhz - blz) : 0.0;
+      const double wlx = uniform_d(blx - m), wly = uniform_d(bly - m), wlz = uniform_d(blz - m);
+      const double whx = uniform_d(bhx + m), why = uniform_d(bhy + m), whz = uniform_d(bhz + m);
+      walk(wlx, wly, wlz, whx, why, whz);
+      if (wb && !overflow) {
+        int32_t* ids = a.wc_ids + (size_t)wid * kWaveCandCap;
+        for (int k = lane; k < nleaf; k += 64) ids[k] = plist[k];
+        if (lane == 0) {
+          wb->lo[0] = wlx;
+          wb->lo[1] = wly;
+          wb->lo[2] = wlz;
+          wb->hi[0] = whx;
+          wb->hi[1] = why;
+          wb->hi[2] = whz;
+          wb->count = nleaf;
+          wb->gen = a.wc_gen;
+        }
+        if (kDbgCounts && a.dbg && lane == 0) atomicAdd(&a.dbg[13], 1ull);
+      }
     }
   }
   if (overflow) join = false;
@@ -534,6 +579,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
           // lockstep over this group's staged pairs (each group's 16-B reads broadcast)
           const float k1_in = k1;
           const int mp = len >> 1;
+          if (kDbgCounts && a.dbg && lane == 0) {
+            atomicAdd(&a.dbg[9], (unsigned long long)(maxc - r0 < S ? maxc - r0 : S));
+            atomicAdd(&a.dbg[10], (unsigned long long)mp);
+            atomicAdd(&a.dbg[11], 1ull);
+          }
 #pragma unroll 1
           for (int k = 0; k < mp; k++) eval2(st4[2 * NG * k], st4[2 * NG * k + 1], 2u * k);
           // the winner of this round, if it improved the lane's best: its index from its slot
@@ -566,6 +616,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
     }
   }
   if (need64) {
+    if (kDbgCounts && a.dbg && lane == 0) atomicAdd(&a.dbg[8], 1ull);
     // Points outside B are farther than r from every joined lane (each ball lies in B), so
     // they can neither be a joined lane's nearest point nor sit in its certificate window.
     // Exact duplicates of the winner (identical coordinates) are not ties: they share its leaf

@@ -260,7 +260,9 @@ def test_fallback_share_small_on_scans(icp, gpu_ctx):
                                    (1_000_000, {"join_factor": 1e6}),
                                    (300_000, {"octree_builder": 1}),
                                    (1_000_000, {"scan_groups": 2}), (1_000_000, {"scan_groups": 4}),
-                                   (300_000, {"xcd_blocks": 0})])
+                                   (300_000, {"xcd_blocks": 0}),
+                                   (1_000_000, {"candidate_cache": 0}), (300_000, {"candidate_margin": 0}),
+                                   (300_000, {"candidate_margin": 256})])
 def test_scan32_matches_fp64_scan(icp, n, cfg):
     """Every configuration of the certified search (fp32 filter scan vs fp64 scan, cell-table
     starts vs root descent, join rule, host-built octree) returns exactly the default's
@@ -286,8 +288,72 @@ def test_scan32_matches_fp64_scan(icp, n, cfg):
         np.testing.assert_array_equal(ia, ib)
         np.testing.assert_array_equal(da, db)
         assert fa == fb
-        if set(cfg) <= {"scan32", "octree_builder", "scan_groups", "xcd_blocks"}:  # the same candidate sets
+        # the same candidate sets (the candidate cache's enlarged boxes overflow other waves)
+        if set(cfg) <= {"scan32", "octree_builder", "scan_groups", "xcd_blocks"}:
             assert ba == bb
+
+
+def test_candidate_cache_motion_and_invalidation(icp):
+    """The wave search's candidate cache (reuse of a wave's enlarged-box candidate list while its
+    new box lies inside) against the cache-free search: small and large motions between iterates
+    (reuse and re-walk), a new target of the same size and a new source (older generations never
+    reused). Correspondences and residuals identical at every step."""
+    rng = np.random.default_rng(21)
+    tgt, src, _ = icp.synth_pair(400_000)
+    tgt2 = tgt[rng.permutation(len(tgt))] * 1.01 + 0.003
+    src2 = src[rng.permutation(len(src))][:300_000] + 0.01
+
+    def rot(deg, t):
+        c, s_ = np.cos(np.radians(deg)), np.sin(np.radians(deg))
+        T = np.eye(4)
+        T[:3, :3] = [[c, -s_, 0], [s_, c, 0], [0, 0, 1]]
+        T[:3, 3] = t
+        return T
+
+    steps = [("iter", None), ("iter", rot(0.01, [0.001, 0, 0])), ("iter", rot(0.01, [0, 0.001, 0])),
+             ("iter", rot(3.0, [0.5, -0.2, 0.1])), ("iter", rot(0.02, [0, 0, 0.001])),
+             ("target", tgt2), ("iter", rot(0.01, [0.001, 0, 0])), ("iter", None),
+             ("source", src2), ("iter", None), ("iter", rot(0.01, [0, 0, 0.002])), ("iter", rot(-5.0, [1.0, 0, 0]))]
+
+    def run(conf):
+        out = []
+        with icp.Context(0, conf) as ctx:
+            ctx.set_target(tgt, 10, 20, icp.RULES_ENGINE)
+            ctx.set_source(src)
+            k = 0
+            for kind, arg in steps:
+                if kind == "target":
+                    ctx.set_target(arg, 10, 20, icp.RULES_ENGINE)
+                elif kind == "source":
+                    ctx.set_source(arg)
+                else:
+                    st = ctx.iterate(arg, k, icp.RULES_ENGINE, 3.0)
+                    k += 1
+                    idx, d = ctx.get_correspondences()
+                    out.append((idx.copy(), d.copy(), st.valid))
+        return out
+
+    a = run({"candidate_cache": 0})
+    b = run({"debug_counters": 0})
+    assert len(a) == len(b) == 10
+    for (ia, da, va), (ib, db, vb) in zip(a, b):
+        np.testing.assert_array_equal(ia, ib)
+        np.testing.assert_array_equal(da, db)
+        assert va == vb
+
+
+def test_candidate_cache_reuses(icp):
+    """After the first iterate, small motions reuse most waves' candidate lists (debug counters)."""
+    tgt, src, _ = icp.synth_pair(500_000)
+    with icp.Context(0, {"debug_counters": 1}) as ctx:
+        ctx.set_target(tgt, 10, 20, icp.RULES_ENGINE)
+        ctx.set_source(src)
+        ctx.iterate(None, 0, icp.RULES_ENGINE, 3.0)
+        c0 = ctx.debug_counters()
+        ctx.iterate(np.eye(4), 1, icp.RULES_ENGINE, 3.0)
+        c1 = ctx.debug_counters()
+    assert c0["cache_hits"] == 0 and c0["cache_stores"] > 0
+    assert c1["cache_hits"] > 0.9 * c0["cache_stores"]
 
 
 def test_scan32_ties_and_self_queries(icp, oracle, golden_nn):
