@@ -109,7 +109,6 @@ static NNLaunch base_launch(const icp_hip_ctx* c) {
   a.cells = c->cells;
   a.cell_lmax = c->cell_lmax;
   a.join_factor = c->cfg.join_factor;
-  a.neg_inf = -__builtin_inff();
   a.xcd_blocks = c->cfg.xcd_blocks;
   a.scan_groups = c->cfg.scan_groups;
   a.dbg = c->dbg;

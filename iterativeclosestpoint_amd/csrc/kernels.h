@@ -64,7 +64,6 @@ struct NNLaunch {
   double root_lo[3], root_hi[3];  // root box (the octree's midpoint recursion starts here)
   unsigned long long* dbg;  // optional diagnostics of the wave search (ICP_DBG_* slots)
   double join_factor;       // a lane joins the wave box if its radius <= this x the mean radius
-  float neg_inf;            // -inf (a launch value: an operand the compiler cannot fold)
   int xcd_blocks;           // renumber the wave search's blocks XCD-contiguously
   int scan_groups;          // lane groups of the fp32 filter scan (1, 2, 4)
   WaveBox* wc_box;          // candidate cache (iterate only; null: every wave walks)

@@ -395,43 +395,53 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
         wave_lds_fence();
       }
   };
+  // a wave that walked B+ stores its list: during the fp32 staging pass only the points inside
+  // B+ (every point the reuse can need), else (no fp32 pass) the whole list after the scan
+  bool wstore = false;
+  double wlx = 0.0, wly = 0.0, wlz = 0.0, whx = 0.0, why = 0.0, whz = 0.0;
+  WaveBox* wb = nullptr;
+  int32_t* wids = nullptr;
   if (__ballot(join) != 0) {
     const uint32_t wid = (uint32_t)__builtin_amdgcn_readfirstlane((int)i) >> 6;
-    WaveBox* wb = a.wc_box ? a.wc_box + wid : nullptr;
+    wb = a.wc_box ? a.wc_box + wid : nullptr;
+    wids = a.wc_ids + (size_t)wid * kWaveCandCap;
     bool reuse = false;
     if (wb)
       reuse = wb->gen == a.wc_gen && blx >= wb->lo[0] && bly >= wb->lo[1] && blz >= wb->lo[2] && bhx <= wb->hi[0] &&
               bhy <= wb->hi[1] && bhz <= wb->hi[2];
     if (reuse) {
       nleaf = wb->count;
-      const int32_t* ids = a.wc_ids + (size_t)wid * kWaveCandCap;
-      for (int k = lane; k < nleaf; k += 64) plist[k] = ids[k];
+      for (int k = lane; k < nleaf; k += 64) plist[k] = wids[k];
       if (kDbgCounts && a.dbg && lane == 0) atomicAdd(&a.dbg[12], 1ull);
     } else {
       // B+ (B itself without the cache); an overflowing B+ makes an overflowing wave (its lanes
       // take the ball search; ~0.06 % of the waves at 10M with the default margin). Wave-uniform
       // doubles are kept in scalar registers.
       const double m = wb ? a.wc_margin * 0.5 * dmax_(dmax_(bhx - blx, bhy - bly), bhz - blz) : 0.0;
-      const double wlx = uniform_d(blx - m), wly = uniform_d(bly - m), wlz = uniform_d(blz - m);
-      const double whx = uniform_d(bhx + m), why = uniform_d(bhy + m), whz = uniform_d(bhz + m);
+      wlx = uniform_d(blx - m);
+      wly = uniform_d(bly - m);
+      wlz = uniform_d(blz - m);
+      whx = uniform_d(bhx + m);
+      why = uniform_d(bhy + m);
+      whz = uniform_d(bhz + m);
       walk(wlx, wly, wlz, whx, why, whz);
-      if (wb && !overflow) {
-        int32_t* ids = a.wc_ids + (size_t)wid * kWaveCandCap;
-        for (int k = lane; k < nleaf; k += 64) ids[k] = plist[k];
-        if (lane == 0) {
-          wb->lo[0] = wlx;
-          wb->lo[1] = wly;
-          wb->lo[2] = wlz;
-          wb->hi[0] = whx;
-          wb->hi[1] = why;
-          wb->hi[2] = whz;
-          wb->count = nleaf;
-          wb->gen = a.wc_gen;
-        }
-        if (kDbgCounts && a.dbg && lane == 0) atomicAdd(&a.dbg[13], 1ull);
-      }
+      wstore = wb && !overflow;
     }
   }
+  // the cache record of a stored list (ids already written)
+  auto store_header = [&](int count) {
+    if (lane == 0) {
+      wb->lo[0] = wlx;
+      wb->lo[1] = wly;
+      wb->lo[2] = wlz;
+      wb->hi[0] = whx;
+      wb->hi[1] = why;
+      wb->hi[2] = whz;
+      wb->count = count;
+      wb->gen = a.wc_gen;
+    }
+    if (kDbgCounts && a.dbg && lane == 0) atomicAdd(&a.dbg[13], 1ull);
+  };
   if (overflow) join = false;
   if (kDbgCounts && a.dbg && lane == 0) {
     atomicAdd(&a.dbg[0], 1ull);
@@ -480,8 +490,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
       // winner is found from its slot once per round. A key is within 63 ulps of its value, and
       // s2 & ~63 is a lower bound of the second-smallest value; keys are finite and >= 0 (offsets
       // <= ext <= 2^60, pads far but finite), so float order is key order.
-      const float ninf = a.neg_inf;  // -inf from the launch record: an opaque med3 operand
       float k1 = __builtin_inff(), k2 = __builtin_inff();
+      int wcount = 0;  // ids stored to the cache (points inside B+)
       int32_t p1 = -1;
       wave_lds_fence();
       double4 nxtp = make_double4(0.0, 0.0, 0.0, 0.0);
@@ -501,7 +511,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
       auto sel = [&](float sq, uint32_t sl) {
         const float key = __uint_as_float((__float_as_uint(sq) & kmask) | sl);
         k2 = __builtin_amdgcn_fmed3f(k1, k2, key);
-        k1 = __builtin_amdgcn_fmed3f(k1, key, ninf);
+        // k1 = min(k1, key) as one VOP2 v_min_f32 (2/3 the issue cost of a VOP3 v_med3_f32 on
+        // gfx950; keys are never NaN, so no canonicalisation is needed)
+        asm("v_min_f32 %0, %1, %2" : "=v"(k1) : "v"(key), "v"(k1));
       };
       auto eval2 = [&](const v4i xy, const v4i zw, uint32_t sl) {
         const f2 X = {__int_as_float(xy.x), __int_as_float(xy.y)};
@@ -515,6 +527,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
       const v4i* st4 = reinterpret_cast<const v4i*>(stage32) + 2 * gq;  // this group's pair 0
       for (int base = 0; base < npts; base += 64) {
         const bool valid = base + lane < npts;
+        if (wstore) {
+          const bool inp = valid && nxtp.x >= wlx && nxtp.x <= whx && nxtp.y >= wly && nxtp.y <= why &&
+                           nxtp.z >= wlz && nxtp.z <= whz;
+          const unsigned long long pm = __ballot(inp);
+          if (inp) wids[wcount + mask_rank(pm)] = (int32_t)__double_as_longlong(nxtp.w);
+          wcount += __popcll(pm);
+        }
         const float vx = (float)(nxtp.x - ocx), vy = (float)(nxtp.y - ocy), vz = (float)(nxtp.z - ocz);
         const float vw = __int_as_float((int)__double_as_longlong(nxtp.w));
         int cn[NG];
@@ -593,6 +612,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
           }
         }
       }
+      if (wstore) {
+        store_header(wcount);
+        wstore = false;
+      }
       const float s2 = __uint_as_float(__float_as_uint(k2) & ~63u);  // <= the second-smallest value
       // fp64 distance of the fp32 winner, exactly as the leaf scan computes it (octree.cpp:139-144)
       double b64 = __builtin_inf();
@@ -614,6 +637,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
         need64 = false;
       }
     }
+  }
+  if (wstore) {  // no fp32 staging pass: the whole list
+    for (int k = lane; k < nleaf; k += 64) wids[k] = plist[k];
+    store_header(nleaf);
   }
   if (need64) {
     if (kDbgCounts && a.dbg && lane == 0) atomicAdd(&a.dbg[8], 1ull);
