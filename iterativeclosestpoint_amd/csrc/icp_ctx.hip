@@ -77,7 +77,7 @@ static void free_source(icp_hip_ctx* c) {
   dfree(c->fb_list);
   dfree(c->fb_u);
   dfree(c->wc_box);
-  dfree(c->wc_ids);
+  dfree(c->wc_ents);
   dfree(c->mparts);
   dfree(c->cparts);
   c->n_src = 0;
@@ -425,7 +425,7 @@ int icp_hip_set_source(icp_hip_ctx* c, const double* xyz, int64_t n) {
   if (c->cfg.candidate_cache && n > 0) {
     const size_t nw = (size_t)((n + 63) / 64);
     HIP_TRY(dalloc(&c->wc_box, nw));
-    HIP_TRY(dalloc(&c->wc_ids, nw * icp::kWaveCandCap));
+    HIP_TRY(dalloc(&c->wc_ents, nw * icp::kWaveCandCap));
     HIP_TRY(hipMemsetAsync(c->wc_box, 0, nw * sizeof(icp::WaveBox), c->stream));  // generation 0: invalid
   }
   c->wc_gen++;
@@ -481,7 +481,7 @@ int icp_hip_iterate(icp_hip_ctx* c, const double* T_apply, int iter, int rules, 
   a.fb_count = c->fb_count;
   a.have_prev = c->have_prev ? 1 : 0;
   a.wc_box = c->wc_box;
-  a.wc_ids = c->wc_ids;
+  a.wc_ents = c->wc_ents;
   a.wc_gen = c->wc_gen;
   a.wc_margin = c->cfg.candidate_margin / 256.0;
   if (!c->lists_zero) HIP_TRY(hipMemsetAsync(c->fb_count, 0, 3 * sizeof(unsigned int), s));

@@ -41,7 +41,7 @@ struct icp_hip_ctx {
   int32_t* fb_list = nullptr;            // exact, ball and per-lane query lists (3 x n_src)
   double* fb_u = nullptr;                // the ball list's distance guesses
   icp::WaveBox* wc_box = nullptr;        // the wave search's candidate cache (one per wave)
-  int32_t* wc_ids = nullptr;
+  float4* wc_ents = nullptr;
   uint32_t wc_gen = 1;                   // bumped by set_target / set_source (records of older
                                          // generations are never reused)
   unsigned int* fb_count = nullptr;

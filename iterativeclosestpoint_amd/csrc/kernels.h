@@ -23,9 +23,11 @@ struct IterDev {
   double pad[4];
 };
 
-// The wave search's candidate cache (one record per wave of 64 queries): the box whose leaves'
+// The wave search's candidate cache (one record per wave of 64 queries): the box B+ whose leaves'
 // points were collected, their count and the generation (target / source upload) it belongs to.
-constexpr int kWaveCandCap = 1008;  // candidate points per wave (the list in LDS; ids in the cache)
+// The entries are the points inside B+ as fp32 offsets from B+'s centre (the scan's own staging
+// values) with the point's id in the fourth word: a reusing wave streams them, no gathers.
+constexpr int kWaveCandCap = 1008;  // candidate points per wave (the walk's list in LDS; the cache)
 struct WaveBox {
   double lo[3];
   double hi[3];
@@ -67,7 +69,7 @@ struct NNLaunch {
   int xcd_blocks;           // renumber the wave search's blocks XCD-contiguously
   int scan_groups;          // lane groups of the fp32 filter scan (1, 2, 4)
   WaveBox* wc_box;          // candidate cache (iterate only; null: every wave walks)
-  int32_t* wc_ids;          // kWaveCandCap candidate ids per wave
+  float4* wc_ents;          // kWaveCandCap entries per wave: (x, y, z) - centre of B+ in fp32, id
   uint32_t wc_gen;          // records of this generation are valid
   double wc_margin;         // a walk collects the leaves of B enlarged by this x B's half-extent
 };

@@ -173,6 +173,17 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
   double qx = 0.0, qy = 0.0, qz = 0.0;
   load_query<APPLY>(a, i, active, qx, qy, qz);
   const bool finite_q = __builtin_isfinite(qx) && __builtin_isfinite(qy) && __builtin_isfinite(qz);
+  // The wave's cache record (7 words on lanes 0..6) and its first 64 entries, loaded with the
+  // query: a reusing wave has its first chunk before the box is known (unused otherwise).
+  const int32_t i0 = __builtin_amdgcn_readfirstlane(i);
+  const uint32_t wid = (uint32_t)i0 >> 6;
+  const bool use_wc = a.wc_box != nullptr && i0 < a.n;
+  double hdr = 0.0;
+  float4 ent0 = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (use_wc) {
+    if (lane < 7) hdr = reinterpret_cast<const double*>(a.wc_box + wid)[lane];
+    ent0 = a.wc_ents[(size_t)wid * kWaveCandCap + lane];
+  }
 
   PCLK(t_p0);
   // Phase 1: the guess (any value is safe: certification also requires best <= u).
@@ -302,10 +313,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
 
   PCLK(t_p2);
   // Phase 3: the leaves meeting B. With the candidate cache (iterate only), a walk collects the
-  // leaves meeting B+ = B enlarged by wc_margin x its largest half-extent per side and stores their
-  // points' ids with B+; the next iterate's wave reuses them without walking while its own B lies
-  // inside B+ (every leaf meeting B then meets B+). Staging filters by B, so the larger list
-  // changes nothing but the staging work.
+  // leaves meeting B+ = B enlarged by wc_margin x its largest half-extent per side and stores the
+  // points inside B+ (as the scan stages them: fp32 offsets from B+'s centre, and the id); the
+  // next iterate's wave streams them back without walking or gathering while its own B lies
+  // inside B+ (every point inside B is then in the list). The scan frame is B+'s centre whenever
+  // the cache is on, so stored and freshly staged offsets are the same values.
   int nleaf = 0;
   bool overflow = false;
   // the cooperative walk over the leaves meeting the box [wl, wh] (wave-uniform)
@@ -395,25 +407,33 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
         wave_lds_fence();
       }
   };
-  // a wave that walked B+ stores its list: during the fp32 staging pass only the points inside
-  // B+ (every point the reuse can need), else (no fp32 pass) the whole list after the scan
-  bool wstore = false;
-  double wlx = 0.0, wly = 0.0, wlz = 0.0, whx = 0.0, why = 0.0, whz = 0.0;
+  bool wstore = false, reuse = false;
+  double wlx = 0.0, wly = 0.0, wlz = 0.0, whx = 0.0, why = 0.0, whz = 0.0;  // B+ of a walk
+  // the frame box: its centre is the scan's origin (B+ with the cache, else B)
+  double flx = blx, fly = bly, flz = blz, fhx = bhx, fhy = bhy, fhz = bhz;
   WaveBox* wb = nullptr;
-  int32_t* wids = nullptr;
+  float4* wents = nullptr;
   if (__ballot(join) != 0) {
-    const uint32_t wid = (uint32_t)__builtin_amdgcn_readfirstlane((int)i) >> 6;
-    wb = a.wc_box ? a.wc_box + wid : nullptr;
-    wids = a.wc_ids + (size_t)wid * kWaveCandCap;
-    bool reuse = false;
-    if (wb)
-      reuse = wb->gen == a.wc_gen && blx >= wb->lo[0] && bly >= wb->lo[1] && blz >= wb->lo[2] && bhx <= wb->hi[0] &&
-              bhy <= wb->hi[1] && bhz <= wb->hi[2];
-    if (reuse) {
-      nleaf = wb->count;
-      for (int k = lane; k < nleaf; k += 64) plist[k] = wids[k];
-      if (kDbgCounts && a.dbg && lane == 0) atomicAdd(&a.dbg[12], 1ull);
-    } else {
+    if (use_wc) {
+      wb = a.wc_box + wid;
+      wents = a.wc_ents + (size_t)wid * kWaveCandCap;
+      const double hlx = readlane_d(hdr, 0), hly = readlane_d(hdr, 1), hlz = readlane_d(hdr, 2);
+      const double hhx = readlane_d(hdr, 3), hhy = readlane_d(hdr, 4), hhz = readlane_d(hdr, 5);
+      const unsigned long long cg = (unsigned long long)__double_as_longlong(readlane_d(hdr, 6));
+      reuse = (uint32_t)(cg >> 32) == a.wc_gen && blx >= hlx && bly >= hly && blz >= hlz && bhx <= hhx &&
+              bhy <= hhy && bhz <= hhz;
+      if (reuse) {
+        nleaf = (int)(uint32_t)cg;
+        flx = hlx;
+        fly = hly;
+        flz = hlz;
+        fhx = hhx;
+        fhy = hhy;
+        fhz = hhz;
+        if (kDbgCounts && a.dbg && lane == 0) atomicAdd(&a.dbg[12], 1ull);
+      }
+    }
+    if (!reuse) {
       // B+ (B itself without the cache); an overflowing B+ makes an overflowing wave (its lanes
       // take the ball search; ~0.06 % of the waves at 10M with the default margin). Wave-uniform
       // doubles are kept in scalar registers.
@@ -426,9 +446,17 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
       whz = uniform_d(bhz + m);
       walk(wlx, wly, wlz, whx, why, whz);
       wstore = wb && !overflow;
+      if (wb) {
+        flx = wlx;
+        fly = wly;
+        flz = wlz;
+        fhx = whx;
+        fhy = why;
+        fhz = whz;
+      }
     }
   }
-  // the cache record of a stored list (ids already written)
+  // the cache record of a stored list (entries already written)
   auto store_header = [&](int count) {
     if (lane == 0) {
       wb->lo[0] = wlx;
@@ -449,22 +477,24 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
   }
 
   PCLK(t_p3);
-  // Phase 4: the lockstep scan: 64 candidates per chunk are gathered by one load per lane (the
-  // next chunk's gather is in flight while the current one is scanned from LDS).
+  // Phase 4: the lockstep scan: 64 candidates per chunk, the next chunk's loads in flight while
+  // the current one is scanned from LDS (a reusing wave streams its cache entries; a walking wave
+  // gathers the points of its list and, with the cache, stores those inside B+).
   double best = __builtin_inf(), second = __builtin_inf();
   int32_t bpos = -1;
   const int npts = nleaf;
   int scanned_pts = 0;
   bool need64 = __ballot(join) != 0 && npts > 0;
+  const double ocx = (flx + fhx) * 0.5, ocy = (fly + fhy) * 0.5, ocz = (flz + fhz) * 0.5;  // scan frame
   if (a.scan32 && need64) {
-    const double ocx = (blx + bhx) * 0.5, ocy = (bly + bhy) * 0.5, ocz = (blz + bhz) * 0.5;
+    // |offset| <= ext for every point inside B and every joined query (B lies in the frame box)
     const double ext = dmax_(dmax_(dmax_(bhx - ocx, ocx - blx), dmax_(bhy - ocy, ocy - bly)),
                              dmax_(bhz - ocz, ocz - blz)) * (1.0 + 0x1p-40);
     if (ext >= 0x1p-40 && ext <= 0x1p60) {
       const float qx32 = (float)(qx - ocx), qy32 = (float)(qy - ocy), qz32 = (float)(qz - ocz);
-      // Group boxes in the scan frame (offsets from B's centre), widened by ext 2^-20: a point
-      // of a joined lane's ball is staged for the lane's group whatever the fp32 rounding of its
-      // offset (<= ext 2^-24). A staged point has |offset| <= ext (1 + 2^-20) (ext_s below).
+      // Group boxes in the scan frame, widened by ext 2^-20: a point of a joined lane's ball is
+      // staged for the lane's group whatever the fp32 rounding of its offset (<= ext 2^-24). A
+      // staged point has |offset| <= ext (1 + 2^-20) (ext_s below).
       const float mg = (float)(ext * 0x1p-20);
       const float dox = (float)(ox_ - ocx), doy = (float)(oy_ - ocy), doz = (float)(oz_ - ocz);
       float gl[NG][3], gh[NG][3];
@@ -491,16 +521,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
       // s2 & ~63 is a lower bound of the second-smallest value; keys are finite and >= 0 (offsets
       // <= ext <= 2^60, pads far but finite), so float order is key order.
       float k1 = __builtin_inff(), k2 = __builtin_inff();
-      int wcount = 0;  // ids stored to the cache (points inside B+)
       int32_t p1 = -1;
-      wave_lds_fence();
-      double4 nxtp = make_double4(0.0, 0.0, 0.0, 0.0);
-      if (lane < npts) {
-        const int32_t g = plist[lane];
-        const TgtPt* p = a.pts + g;
-        const double2 xy = *reinterpret_cast<const double2*>(&p->x);
-        nxtp = make_double4(xy.x, xy.y, p->z, __longlong_as_double((long long)g));
-      }
       typedef float f2 __attribute__((ext_vector_type(2)));
       typedef int v4i __attribute__((ext_vector_type(4)));
       const f2 qx2 = {qx32, qx32}, qy2 = {qy32, qy32}, qz2 = {qz32, qz32};
@@ -525,22 +546,15 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
         sel(sq.y, (uint32_t)__builtin_amdgcn_readfirstlane((int)(sl + 1u)));  // a scalar operand
       };
       const v4i* st4 = reinterpret_cast<const v4i*>(stage32) + 2 * gq;  // this group's pair 0
-      for (int base = 0; base < npts; base += 64) {
+      // One chunk of 64 candidates (lane = candidate base + lane; offsets vx, vy, vz, id bits vw):
+      // group membership, rank among the group's points of the chunk, and (first round) the store
+      // into the group's segment; `next` issues the following chunk's loads once this one is
+      // staged; then the lockstep scan. Later rounds (more than S points of one group in one
+      // chunk, rare) test again rather than keep NG ranks and masks live.
+      auto chunk = [&](int base, float vx, float vy, float vz, float vw, auto&& next) {
         const bool valid = base + lane < npts;
-        if (wstore) {
-          const bool inp = valid && nxtp.x >= wlx && nxtp.x <= whx && nxtp.y >= wly && nxtp.y <= why &&
-                           nxtp.z >= wlz && nxtp.z <= whz;
-          const unsigned long long pm = __ballot(inp);
-          if (inp) wids[wcount + mask_rank(pm)] = (int32_t)__double_as_longlong(nxtp.w);
-          wcount += __popcll(pm);
-        }
-        const float vx = (float)(nxtp.x - ocx), vy = (float)(nxtp.y - ocy), vz = (float)(nxtp.z - ocz);
-        const float vw = __int_as_float((int)__double_as_longlong(nxtp.w));
         int cn[NG];
         int maxc = 0;
-        // group membership, rank among the group's points of the chunk, and (first round) the
-        // store into the group's segment; later rounds (more than S points of one group in one
-        // chunk, rare) test again rather than keep NG ranks and masks live
         auto stage_round = [&](int r0, bool count) {
 #pragma unroll
           for (int g = 0; g < NG; g++) {
@@ -565,13 +579,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
         stage_round(0, true);
 #pragma unroll
         for (int g = 0; g < NG; g++) scanned_pts += cn[g];
-        const int nb = base + 64;
-        if (nb + lane < npts) {
-          const int32_t g = plist[nb + lane];
-          const TgtPt* p = a.pts + g;
-          const double2 xy = *reinterpret_cast<const double2*>(&p->x);
-          nxtp = make_double4(xy.x, xy.y, p->z, __longlong_as_double((long long)g));
-        }
+        next();
         for (int r0 = 0; r0 < maxc; r0 += S) {
           if (r0 > 0) {
             wave_lds_fence();
@@ -611,10 +619,49 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
             p1 = __float_as_int(stage32[8 * ((sl >> 1) * NG + gq) + 6 + (sl & 1u)]);
           }
         }
-      }
-      if (wstore) {
-        store_header(wcount);
-        wstore = false;
+      };
+      wave_lds_fence();
+      if (reuse) {
+        float4 nx = ent0;  // loaded with the query
+        for (int base = 0; base < npts; base += 64) {
+          const float vx = nx.x, vy = nx.y, vz = nx.z, vw = nx.w;
+          chunk(base, vx, vy, vz, vw, [&]() {
+            if (base + 64 + lane < npts) nx = wents[base + 64 + lane];
+          });
+        }
+      } else {
+        int wcount = 0;  // entries stored to the cache (points inside B+)
+        double4 nxtp = make_double4(0.0, 0.0, 0.0, 0.0);
+        if (lane < npts) {
+          const int32_t g = plist[lane];
+          const TgtPt* p = a.pts + g;
+          const double2 xy = *reinterpret_cast<const double2*>(&p->x);
+          nxtp = make_double4(xy.x, xy.y, p->z, __longlong_as_double((long long)g));
+        }
+        for (int base = 0; base < npts; base += 64) {
+          const float vx = (float)(nxtp.x - ocx), vy = (float)(nxtp.y - ocy), vz = (float)(nxtp.z - ocz);
+          const float vw = __int_as_float((int)__double_as_longlong(nxtp.w));
+          if (wstore) {
+            const bool inp = base + lane < npts && nxtp.x >= wlx && nxtp.x <= whx && nxtp.y >= wly &&
+                             nxtp.y <= why && nxtp.z >= wlz && nxtp.z <= whz;
+            const unsigned long long pm = __ballot(inp);
+            if (inp) wents[wcount + mask_rank(pm)] = make_float4(vx, vy, vz, vw);
+            wcount += __popcll(pm);
+          }
+          chunk(base, vx, vy, vz, vw, [&]() {
+            const int nb = base + 64;
+            if (nb + lane < npts) {
+              const int32_t g = plist[nb + lane];
+              const TgtPt* p = a.pts + g;
+              const double2 xy = *reinterpret_cast<const double2*>(&p->x);
+              nxtp = make_double4(xy.x, xy.y, p->z, __longlong_as_double((long long)g));
+            }
+          });
+        }
+        if (wstore) {
+          store_header(wcount);
+          wstore = false;
+        }
       }
       const float s2 = __uint_as_float(__float_as_uint(k2) & ~63u);  // <= the second-smallest value
       // fp64 distance of the fp32 winner, exactly as the leaf scan computes it (octree.cpp:139-144)
@@ -638,9 +685,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
       }
     }
   }
-  if (wstore) {  // no fp32 staging pass: the whole list
-    for (int k = lane; k < nleaf; k += 64) wids[k] = plist[k];
-    store_header(nleaf);
+  if (wstore && npts == 0) {  // an empty list (no scan below)
+    store_header(0);
+    wstore = false;
   }
   if (need64) {
     if (kDbgCounts && a.dbg && lane == 0) atomicAdd(&a.dbg[8], 1ull);
@@ -653,21 +700,33 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
     wave_lds_fence();
     double4 nxtp = make_double4(0.0, 0.0, 0.0, 0.0);
     bool nin = false;
+    // candidate k: from the walk's list, or the id word of a reused cache entry
+    auto cand_id = [&](int k) { return reuse ? reinterpret_cast<const int32_t*>(wents + k)[3] : plist[k]; };
     if (lane < npts) {
-      const int32_t g = plist[lane];
+      const int32_t g = cand_id(lane);
       const TgtPt* p = a.pts + g;
       const double2 xy = *reinterpret_cast<const double2*>(&p->x);
       nxtp = make_double4(xy.x, xy.y, p->z, __longlong_as_double((long long)g));
     }
+    int wcount = 0;  // a walking wave without an fp32 pass stores its entries here
     for (int base = 0; base < npts; base += 64) {
       nin = base + lane < npts && nxtp.x >= blx && nxtp.x <= bhx && nxtp.y >= bly && nxtp.y <= bhy &&
             nxtp.z >= blz && nxtp.z <= bhz;
       const unsigned long long im = __ballot(nin);
       const int slot = mask_rank(im);
       const double4 cur = nxtp;
+      if (wstore) {
+        const bool inp = base + lane < npts && cur.x >= wlx && cur.x <= whx && cur.y >= wly && cur.y <= why &&
+                         cur.z >= wlz && cur.z <= whz;
+        const unsigned long long pm = __ballot(inp);
+        if (inp)
+          wents[wcount + mask_rank(pm)] = make_float4((float)(cur.x - ocx), (float)(cur.y - ocy), (float)(cur.z - ocz),
+                                                      __int_as_float((int)__double_as_longlong(cur.w)));
+        wcount += __popcll(pm);
+      }
       const int nb = base + 64;
       if (nb + lane < npts) {
-        const int32_t g = plist[nb + lane];
+        const int32_t g = cand_id(nb + lane);
         const TgtPt* p = a.pts + g;
         const double2 xy = *reinterpret_cast<const double2*>(&p->x);
         nxtp = make_double4(xy.x, xy.y, p->z, __longlong_as_double((long long)g));
@@ -701,6 +760,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
           }
         }
       }
+    }
+    if (wstore) {
+      store_header(wcount);
+      wstore = false;
     }
     if (kDbgCounts && a.dbg && lane == 0) atomicAdd(&a.dbg[4], (unsigned long long)scanned_pts);
   }
