@@ -69,7 +69,7 @@ typedef struct icp_hip_config {
   int32_t scan_groups;    /* 1, 2 or 4: the fp32 filter scan of a wave splits its lanes into this
                              many kd sub-buckets, each scanning only the candidates inside its
                              own box (fewer distance evaluations per query, more staging
-                             work: measured neutral at 2, slower at 4 on config 4)        dflt 1 */
+                             work: 7 % faster at 2, slower at 4 on config 4)             dflt 2 */
   int32_t candidate_cache;  /* 1: each wave of the iterate's search keeps the candidate list of
                                its search box B enlarged by candidate_margin (1/256 units of B's
                                largest half-extent per side), and the next iterate reuses it
