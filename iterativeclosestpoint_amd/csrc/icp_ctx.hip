@@ -506,7 +506,6 @@ int icp_hip_iterate(icp_hip_ctx* c, const double* T_apply, int iter, int rules, 
   cl.y = c->y;
   cl.z = c->z;
   cl.pos = c->pos;
-  cl.dist = c->dist;
   cl.pts = c->pts;
   cl.it = c->it;
   cl.part = c->cparts;

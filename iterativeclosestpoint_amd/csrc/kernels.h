@@ -109,7 +109,6 @@ struct CullLaunch {
   const double* y;
   const double* z;
   const int32_t* pos;
-  const double* dist;
   const TgtPt* pts;
   const IterDev* it;
   CovMoments* part;

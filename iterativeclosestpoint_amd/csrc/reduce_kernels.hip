@@ -281,9 +281,11 @@ __global__ void __launch_bounds__(64) k_finalize_cov(const CovMoments* gathered,
 }
 
 // 3-sigma cull + covariance sums. One thread per 4 queries (1024 per block). A thread first
-// issues all its streamed loads (d, pos, x, y, z of its 4 queries), then all 4 match gathers (a
-// culled query gathers point 0, always valid), then accumulates in query order: two dependent
-// memory round trips instead of three.
+// issues all its streamed loads (pos, x, y, z of its 4 queries), then all 4 match gathers, then
+// accumulates in query order: two dependent memory round trips. The residual is not read: every
+// search path stores d = sqrt(fl(dx^2 + dy^2 + dz^2)) of the query and its match (nn_device.h,
+// octree.cpp:139-144 arithmetic; a non-finite query's default match included), so the same
+// operations on the same operands give its bits again (8 of 68 B per query not streamed).
 constexpr int kCullPer = 4;
 
 __global__ void __launch_bounds__(256) k_cull_cov(CullLaunch a) {
@@ -296,13 +298,12 @@ __global__ void __launch_bounds__(256) k_cull_cov(CullLaunch a) {
   double v[17];
 #pragma unroll
   for (int k = 0; k < 17; k++) v[k] = 0.0;
-  double dq[kCullPer], qx[kCullPer], qy[kCullPer], qz[kCullPer];
+  double qx[kCullPer], qy[kCullPer], qz[kCullPer];
   int32_t pq[kCullPer];
 #pragma unroll
   for (int e = 0; e < kCullPer; e++) {
     const int64_t i = base + e * 256;
     const bool in = i < a.n;
-    dq[e] = in ? a.dist[i] : __builtin_nan("");  // NaN <= thr is false: not a valid pair
     pq[e] = in ? a.pos[i] : 0;
     qx[e] = in ? a.x[i] : 0.0;
     qy[e] = in ? a.y[i] : 0.0;
@@ -311,7 +312,7 @@ __global__ void __launch_bounds__(256) k_cull_cov(CullLaunch a) {
   double mx[kCullPer], my[kCullPer], mz[kCullPer];
 #pragma unroll
   for (int e = 0; e < kCullPer; e++) {
-    const TgtPt* p = a.pts + (dq[e] <= thr ? pq[e] : 0);
+    const TgtPt* p = a.pts + pq[e];
     const double2 pxy = *reinterpret_cast<const double2*>(&p->x);
     mx[e] = pxy.x;
     my[e] = pxy.y;
@@ -319,7 +320,9 @@ __global__ void __launch_bounds__(256) k_cull_cov(CullLaunch a) {
   }
 #pragma unroll
   for (int e = 0; e < kCullPer; e++) {
-    const double d = dq[e];
+    const double ex = mx[e] - qx[e], ey = my[e] - qy[e], ez = mz[e] - qz[e];
+    // the stored residual, bit for bit (NaN past the end: NaN <= thr is false)
+    const double d = base + e * 256 < a.n ? __builtin_sqrt(ex * ex + ey * ey + ez * ez) : __builtin_nan("");
     if (d <= thr) {  // icpengine.cpp:265
       const double da[3] = {qx[e] - sh[0], qy[e] - sh[1], qz[e] - sh[2]};
       const double db[3] = {mx[e] - sh[3], my[e] - sh[4], mz[e] - sh[5]};
