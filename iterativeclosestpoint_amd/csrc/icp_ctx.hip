@@ -176,8 +176,10 @@ int icp_hip_create_ex(icp_hip_ctx** out, int device, const icp_hip_config* cfg) 
     return fail(ICP_HIP_EDEVICE, "hipStreamCreate failed");
   }
   for (hipEvent_t* ev : {&c->ev_it0, &c->ev_it1}) (void)hipEventCreate(ev);
+  // The per-iterate timing ring only measures elapsed times: no system-scope fence on record
+  // (a default event's release writes back L2, ~5 us of GPU idle per record between kernels).
   for (auto& r : c->ring)
-    for (hipEvent_t& ev : r) (void)hipEventCreate(&ev);
+    for (hipEvent_t& ev : r) (void)hipEventCreateWithFlags(&ev, hipEventDisableSystemFence);
   if (dalloc(&c->it, 1) != hipSuccess ||
       hipHostMalloc(reinterpret_cast<void**>(&c->h_it), sizeof(IterDev), hipHostMallocMapped | hipHostMallocCoherent) !=
           hipSuccess ||
