@@ -14,7 +14,7 @@ Rank 0 prints ONE JSON line. `value` = the points of all ranks x K / the wall ti
 iterations (max over ranks); `median` = the same rate from the median iteration of 2..K
 (SURVEY.md §8d). Extra objects:
   roofline      the search kernel k_nn_wave: its compulsory HBM bytes per launch (DESIGN.md §5:
-                68 B per query streamed + every target point (28 B) and node (56 B) once) / its
+                64 B per query streamed + every target point (28 B) and node (56 B) once) / its
                 average HIP-event duration over the timed iterations; `traffic` = PMC bytes per
                 launch (rocprofv3, calibrated per access width: tools/calib_pmc.sh) of the same
                 kernel source, or null.
@@ -52,7 +52,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
 CONFIG_NAMES = {100_000: "config2", 1_000_000: "config3-size", 10_000_000: "config4", 50_000_000: "config5"}
 SEARCH_SOURCES = ("nn_kernels.hip", "nn_device.h", "kernels.h")
 # compulsory bytes of one k_nn_wave<true> launch
-STREAM_B_PER_QUERY = 24 + 24 + 8 + 4 + 8  # source read + transformed write, guess, pos + dist
+STREAM_B_PER_QUERY = 24 + 24 + 4 + 4 + 8  # source read + transformed write, previous match (guess), pos + dist
 TGT_B_PER_POINT = 28  # x, y, z + original index of a leaf-ordered target point
 NODE_B = 56  # box (48 B) + topology (8 B) of a node record
 

@@ -76,7 +76,7 @@ typedef struct icp_hip_config {
                                without walking the octree while its new box lies inside
                                (an exact containment test: results are unchanged); 0: every
                                iterate walks                                              dflt 1 */
-  int32_t candidate_margin; /* see candidate_cache, in [0, 1024]                         dflt 8 */
+  int32_t candidate_margin; /* see candidate_cache, in [0, 1024]                        dflt 16 */
   int32_t reserved[3];    /* zero */
 } icp_hip_config;
 

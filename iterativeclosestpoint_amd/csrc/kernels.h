@@ -72,6 +72,7 @@ struct NNLaunch {
   float4* wc_ents;          // kWaveCandCap entries per wave: (x, y, z) - centre of B+ in fp32, id
   uint32_t wc_gen;          // records of this generation are valid
   double wc_margin;         // a walk collects the leaves of B enlarged by this x B's half-extent
+  double wc_loose;          // a record is reused only while vol(B+) <= this x vol(B)
 };
 
 // Threads per block of the per-thread search kernels for a given stack depth.

@@ -420,8 +420,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
       const double hlx = readlane_d(hdr, 0), hly = readlane_d(hdr, 1), hlz = readlane_d(hdr, 2);
       const double hhx = readlane_d(hdr, 3), hhy = readlane_d(hdr, 4), hhz = readlane_d(hdr, 5);
       const unsigned long long cg = (unsigned long long)__double_as_longlong(readlane_d(hdr, 6));
+      // reused while B lies inside B+ and B+ is not much larger than B (a wave whose box shrank,
+      // e.g. after the first iterate's descent guesses, walks again and stores a tighter list)
       reuse = (uint32_t)(cg >> 32) == a.wc_gen && blx >= hlx && bly >= hly && blz >= hlz && bhx <= hhx &&
-              bhy <= hhy && bhz <= hhz;
+              bhy <= hhy && bhz <= hhz &&
+              (hhx - hlx) * (hhy - hly) * (hhz - hlz) <= a.wc_loose * ((bhx - blx) * (bhy - bly) * (bhz - blz));
       if (reuse) {
         nleaf = (int)(uint32_t)cg;
         flx = hlx;
