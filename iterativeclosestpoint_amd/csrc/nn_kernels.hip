@@ -440,7 +440,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
       // B+ (B itself without the cache); an overflowing B+ makes an overflowing wave (its lanes
       // take the ball search; ~0.06 % of the waves at 10M with the default margin). Wave-uniform
       // doubles are kept in scalar registers.
-      const double m = wb ? a.wc_margin * 0.5 * dmax_(dmax_(bhx - blx, bhy - bly), bhz - blz) : 0.0;
+      // Without previous residuals (descent guesses: large, loose boxes that the next iterate
+      // re-walks anyway) the wave walks B itself and stores nothing.
+      const bool keep = wb && a.have_prev;
+      const double m = keep ? a.wc_margin * 0.5 * dmax_(dmax_(bhx - blx, bhy - bly), bhz - blz) : 0.0;
       wlx = uniform_d(blx - m);
       wly = uniform_d(bly - m);
       wlz = uniform_d(blz - m);
@@ -448,8 +451,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
       why = uniform_d(bhy + m);
       whz = uniform_d(bhz + m);
       walk(wlx, wly, wlz, whx, why, whz);
-      wstore = wb && !overflow;
-      if (wb) {
+      wstore = keep && !overflow;
+      if (keep) {
         flx = wlx;
         fly = wly;
         flz = wlz;

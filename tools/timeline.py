@@ -25,3 +25,15 @@ if len(starts) >= 3:
         s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
         print(f"  {(s - t0) / 1e3:8.1f} {(e - s) / 1e3:8.1f} {(s - prev_end) / 1e3:7.1f}  {r['Kernel_Name'][:70]}")
         prev_end = e
+# the first iterate of each session (k_nn_wave<false, ...>: no previous residuals)
+firsts = [i for i, r in enumerate(rows) if "k_nn_wave<false" in r["Kernel_Name"]]
+for a in firsts:
+    nxt = [i for i in starts if i > a]
+    b = nxt[0] if nxt else len(rows) - 1
+    t0 = int(rows[a]["Start_Timestamp"])
+    prev_end = t0
+    print("timeline of a first iterate (us): start  dur  gap-before  kernel")
+    for r in rows[a:b + 1]:
+        s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+        print(f"  {(s - t0) / 1e3:8.1f} {(e - s) / 1e3:8.1f} {(s - prev_end) / 1e3:7.1f}  {r['Kernel_Name'][:70]}")
+        prev_end = e
