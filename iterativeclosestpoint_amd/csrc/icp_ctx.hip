@@ -469,7 +469,6 @@ int icp_hip_iterate(icp_hip_ctx* c, const double* T_apply, int iter, int rules, 
   HIP_TRY(hipSetDevice(c->device));
   hipStream_t s = c->stream;
   hipEvent_t* ev = c->ring[c->n_iterates % icp_hip_ctx::kTimingRing];
-  HIP_TRY(hipEventRecord(ev[0], s));
   NNLaunch a = base_launch(c);
   a.x = c->x;
   a.y = c->y;
@@ -494,8 +493,8 @@ int icp_hip_iterate(icp_hip_ctx* c, const double* T_apply, int iter, int rules, 
   if (!c->lists_zero) HIP_TRY(hipMemsetAsync(c->fb_count, 0, 3 * sizeof(unsigned int), s));
   c->lists_zero = false;
   if (c->dbg) HIP_TRY(hipMemsetAsync(c->dbg, 0, ICP_DBG_SLOTS * sizeof(unsigned long long), s));
-  HIP_TRY(hipEventRecord(ev[1], s));
-  a.ev_fast_done = ev[2];
+  a.ev_start = ev[0];
+  a.ev_fast_done = ev[1];
   HIP_TRY(launch_nn(a, s));
   // residual moments -> mean, std, threshold (no communicator: fused into the last merge level)
   const bool multi = c->comm != nullptr || c->xfn != nullptr;
@@ -528,7 +527,7 @@ int icp_hip_iterate(icp_hip_ctx* c, const double* T_apply, int iter, int rules, 
     if (rc != ICP_HIP_OK) return rc;
     HIP_TRY(launch_finalize_cov(c->gc, c->nranks, c->it, pub, s));
   }
-  HIP_TRY(hipEventRecord(ev[3], s));
+  HIP_TRY(hipEventRecord(ev[2], s));
   c->n_iterates++;
   // The host's only wait of the iteration: the publishing kernel stores the record with
   // system-scope stores, waits for their acknowledgement, then stores the sequence word (no
@@ -717,10 +716,10 @@ int icp_hip_timings(icp_hip_ctx* c, int k, double* nn_ms, double* it_ms) {
   HIP_TRY(hipSetDevice(c->device));
   for (int j = 0; j < k; j++) {
     hipEvent_t* ev = c->ring[(c->n_iterates - k + j) % icp_hip_ctx::kTimingRing];
-    HIP_TRY(hipEventSynchronize(ev[3]));
+    HIP_TRY(hipEventSynchronize(ev[2]));
     float a = 0.f, b = 0.f;
-    HIP_TRY(hipEventElapsedTime(&a, ev[1], ev[2]));
-    HIP_TRY(hipEventElapsedTime(&b, ev[0], ev[3]));
+    HIP_TRY(hipEventElapsedTime(&a, ev[0], ev[1]));
+    HIP_TRY(hipEventElapsedTime(&b, ev[0], ev[2]));
     if (nn_ms) nn_ms[j] = a;
     if (it_ms) it_ms[j] = b;
   }

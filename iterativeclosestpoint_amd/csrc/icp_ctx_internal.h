@@ -15,9 +15,9 @@ struct icp_hip_ctx {
   hipStream_t stream = nullptr;
   hipEvent_t ev_it0 = nullptr, ev_it1 = nullptr;  // set_target timing
   // per-iterate timing events, a ring over the last kTimingRing iterates:
-  // [0] iterate start, [1] search start, [2] search kernel done, [3] iterate end
+  // [0] search start (the iterate's first launch), [1] search kernel done, [2] iterate end
   static constexpr int kTimingRing = 256;
-  hipEvent_t ring[kTimingRing][4] = {};
+  hipEvent_t ring[kTimingRing][3] = {};
   int64_t n_iterates = 0;
 
   // target (replicated on every rank)

@@ -58,7 +58,8 @@ struct NNLaunch {
   double* fb_u2;            // the distance guess u of each fb_list2 entry
   int32_t* fb_list3;        // queries left to the per-lane certified search
   unsigned int* fb_count;   // [0] exact, [1] ball, [2] per-lane list sizes; zero at the launch
-  hipEvent_t ev_fast_done;  // optional: recorded right after the main search kernel
+  hipEvent_t ev_start;      // optional: the main search kernel's start and end, recorded by its
+  hipEvent_t ev_fast_done;  // own dispatch (hipExtLaunchKernel: no marker packets between kernels)
   int have_prev;            // dist_out holds the previous residuals of these queries
   int scan32;               // fp32 filter scan with fp64 certification (0: fp64 scan)
   const int32_t* cells;     // per-level cell tables (octree_gpu.h), null = root descent

@@ -14,6 +14,7 @@
 //
 // Everything is fp64 except the scan's filter, whose result is re-evaluated in fp64; built with
 // -ffp-contract=off (the reference is built without FMA).
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <cstddef>
@@ -1025,6 +1026,7 @@ hipError_t launch_nn(const NNLaunch& a, hipStream_t s) {
   if (shmem < 1024) shmem = 1024;  // also hosts the block reduction
   const unsigned grid = grid_for(a.n, bs);
   if (a.search == ICP_SEARCH_REFERENCE || a.count) {
+    if (a.ev_start) (void)hipEventRecord(a.ev_start, s);
     if (a.apply) {
       if (a.count) hipLaunchKernelGGL((k_nn_ref<true, true>), dim3(grid), dim3(bs), shmem, s, a);
       else hipLaunchKernelGGL((k_nn_ref<true, false>), dim3(grid), dim3(bs), shmem, s, a);
@@ -1038,16 +1040,19 @@ hipError_t launch_nn(const NNLaunch& a, hipStream_t s) {
   // wave search -> ball search -> per-lane search / exact DFS
   const unsigned wgrid = grid_for(a.n, 256);
   const size_t wshm = (size_t)(256 / 64) * kWaveLds;
+  // the kernel's own dispatch records the timing events (null events: a plain launch)
+  auto wave = [&](auto kern) {
+    hipExtLaunchKernelGGL(kern, dim3(wgrid), dim3(256), (uint32_t)wshm, s, a.ev_start, a.ev_fast_done, 0u, a);
+  };
   switch ((a.apply ? 8 : 0) + a.scan_groups) {
-    case 9: hipLaunchKernelGGL((k_nn_wave<true, 1>), dim3(wgrid), dim3(256), wshm, s, a); break;
-    case 10: hipLaunchKernelGGL((k_nn_wave<true, 2>), dim3(wgrid), dim3(256), wshm, s, a); break;
-    case 12: hipLaunchKernelGGL((k_nn_wave<true, 4>), dim3(wgrid), dim3(256), wshm, s, a); break;
-    case 1: hipLaunchKernelGGL((k_nn_wave<false, 1>), dim3(wgrid), dim3(256), wshm, s, a); break;
-    case 2: hipLaunchKernelGGL((k_nn_wave<false, 2>), dim3(wgrid), dim3(256), wshm, s, a); break;
-    case 4: hipLaunchKernelGGL((k_nn_wave<false, 4>), dim3(wgrid), dim3(256), wshm, s, a); break;
+    case 9: wave(k_nn_wave<true, 1>); break;
+    case 10: wave(k_nn_wave<true, 2>); break;
+    case 12: wave(k_nn_wave<true, 4>); break;
+    case 1: wave(k_nn_wave<false, 1>); break;
+    case 2: wave(k_nn_wave<false, 2>); break;
+    case 4: wave(k_nn_wave<false, 4>); break;
     default: return hipErrorInvalidValue;
   }
-  if (a.ev_fast_done) (void)hipEventRecord(a.ev_fast_done, s);
   // the lists are short (usually empty after the first iteration): small grids of 64-thread
   // blocks, grid-stride over the list
   const int64_t bq = (a.n + kBallGroups - 1) / kBallGroups;
