@@ -17,7 +17,8 @@ iterations (max over ranks); `median` = the same rate from the median iteration 
                 64 B per query streamed + every target point (28 B) and node (56 B) once) / its
                 average HIP-event duration over the timed iterations; `traffic` = PMC bytes per
                 launch (rocprofv3, calibrated per access width: tools/calib_pmc.sh) of the same
-                kernel source, or null.
+                kernel source, or null; `traffic_gbs` / `traffic_frac` = those bytes over this
+                run's kernel time, against the peak.
   reference_work  SURVEY.md §8d's model of the reference DFS's work (148 + 56 V + 24 P bytes per
                 correspondence): what the reference would move, not what this kernel moves.
   cpu_baseline  the REFERENCE CPU path (oracle/_ref/ref_bench: icp_registration.cpp's ICP()),
@@ -391,6 +392,10 @@ def main() -> int:
                 "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "traffic_over_algorithmic": None if traffic is None else round(traffic / need, 3),
+                # the PMC-measured HBM rate of the same launch (the profiled bytes over this run's
+                # kernel time) against the peak: the north star's "rocprof-measured GB/s"
+                "traffic_gbs": None if traffic is None else round(traffic / nn_avg_s / 1e9, 1),
+                "traffic_frac": None if traffic is None else round(traffic / nn_avg_s / 1e9 / HBM_PEAK_GBS, 4),
                 "kernel": "k_nn_wave<true> (fused transform + wave-cooperative certified octree NN + residual)",
                 "algorithmic_bytes_per_launch": round(need), "kernel_ms_avg": round(float(np.mean(nn_ms)), 4),
                 "iterate_device_ms_avg": round(float(np.mean(it_ms)), 4),
