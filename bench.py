@@ -247,7 +247,9 @@ def main() -> int:
 
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        with stdout_to_stderr():  # gloo prints "[Gloo] Rank r is connected to ..." on fd 1
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+            dist.barrier()
     n_dev = max(1, torch.cuda.device_count())
     device = local_rank % n_dev  # ranks > GPUs only in host-exchange rehearsals
     gpus_used = min(world, n_dev)
