@@ -27,6 +27,9 @@
 #ifndef ICP_PHASE_CLOCKS
 #define ICP_PHASE_CLOCKS 0
 #endif
+#ifndef ICP_SHRINK_RETRY
+#define ICP_SHRINK_RETRY 1
+#endif
 constexpr bool kDbgCounts = !ICP_PHASE_CLOCKS;  // the clock build counts nothing (no atomics)
 #if ICP_PHASE_CLOCKS
 #define PCLK(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
@@ -452,6 +455,18 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
       why = uniform_d(bhy + m);
       whz = uniform_d(bhz + m);
       walk(wlx, wly, wlz, whx, why, whz);
+      if (ICP_SHRINK_RETRY && overflow && keep) {
+        // B+ holds too many points: walk again with a quarter of the margin and store that list
+        // (an overflowing wave that stored nothing would overflow again at every iterate)
+        const double m4 = 0.25 * m;
+        wlx = uniform_d(blx - m4);
+        wly = uniform_d(bly - m4);
+        wlz = uniform_d(blz - m4);
+        whx = uniform_d(bhx + m4);
+        why = uniform_d(bhy + m4);
+        whz = uniform_d(bhz + m4);
+        walk(wlx, wly, wlz, whx, why, whz);
+      }
       wstore = keep && !overflow;
       if (keep) {
         flx = wlx;
