@@ -188,13 +188,13 @@ int icp_hip_create_ex(icp_hip_ctx** out, int device, const icp_hip_config* cfg) 
       hipHostMalloc(reinterpret_cast<void**>(&c->h_it), sizeof(IterDev), hipHostMallocMapped | hipHostMallocCoherent) !=
           hipSuccess ||
       hipHostGetDevicePointer(reinterpret_cast<void**>(&c->h_it_dev), c->h_it, 0) != hipSuccess ||
-      dalloc(&c->counters, 2) != hipSuccess || dalloc(&c->fb_count, 3) != hipSuccess ||
+      dalloc(&c->counters, 2) != hipSuccess || dalloc(&c->fb_count, 4) != hipSuccess ||
       (conf.debug_counters && dalloc(&c->dbg, ICP_DBG_SLOTS) != hipSuccess)) {
     icp_hip_destroy(c);
     return fail(ICP_HIP_ENOMEM, "context allocation failed");
   }
   (void)hipMemset(c->it, 0, sizeof(IterDev));
-  (void)hipMemset(c->fb_count, 0, 3 * sizeof(unsigned int));
+  (void)hipMemset(c->fb_count, 0, 4 * sizeof(unsigned int));
   if (c->dbg) (void)hipMemset(c->dbg, 0, ICP_DBG_SLOTS * sizeof(unsigned long long));
   std::memset(c->h_it, 0, sizeof(IterDev));
   c->lists_zero = true;
@@ -481,7 +481,6 @@ int icp_hip_iterate(icp_hip_ctx* c, const double* T_apply, int iter, int rules, 
     for (int k = 0; k < 12; k++) a.T[k] = T_apply[k];
   a.fb_list = c->fb_list;
   a.fb_list2 = c->fb_list + c->n_src;
-  a.fb_list3 = c->fb_list + 2 * c->n_src;
   a.fb_u2 = c->fb_u;
   a.fb_count = c->fb_count;
   a.have_prev = c->have_prev ? 1 : 0;
@@ -490,7 +489,7 @@ int icp_hip_iterate(icp_hip_ctx* c, const double* T_apply, int iter, int rules, 
   a.wc_gen = c->wc_gen;
   a.wc_margin = c->cfg.candidate_margin / 256.0;
   a.wc_loose = kCacheLoose;
-  if (!c->lists_zero) HIP_TRY(hipMemsetAsync(c->fb_count, 0, 3 * sizeof(unsigned int), s));
+  if (!c->lists_zero) HIP_TRY(hipMemsetAsync(c->fb_count, 0, 4 * sizeof(unsigned int), s));
   c->lists_zero = false;
   if (c->dbg) HIP_TRY(hipMemsetAsync(c->dbg, 0, ICP_DBG_SLOTS * sizeof(unsigned long long), s));
   a.ev_start = ev[0];
@@ -656,15 +655,18 @@ int icp_hip_nn(icp_hip_ctx* c, const double* q, int64_t n, int32_t* idx_out, dou
     if (e == hipSuccess) e = dalloc(&fbu, (size_t)n);
     a.fb_list = fbl;
     a.fb_list2 = fbl + n;
-    a.fb_list3 = fbl + 2 * n;
     a.fb_u2 = fbu;
     a.fb_count = c->fb_count;
-    if (e == hipSuccess) e = hipMemsetAsync(c->fb_count, 0, 3 * sizeof(unsigned int), c->stream);
+    unsigned int lists4[4] = {0, 0, 0, 0};
+    if (e == hipSuccess) e = hipMemsetAsync(c->fb_count, 0, 4 * sizeof(unsigned int), c->stream);
     c->lists_zero = false;
     if (e == hipSuccess) e = launch_nn(a, c->stream);
     if (e == hipSuccess)
-      e = hipMemcpyAsync(c->last_lists, c->fb_count, 3 * sizeof(unsigned int), hipMemcpyDeviceToHost, c->stream);
+      e = hipMemcpyAsync(lists4, c->fb_count, 4 * sizeof(unsigned int), hipMemcpyDeviceToHost, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    c->last_lists[0] = lists4[0] + lists4[3];  // exact: the wave search's list + the ball's DFS finishes
+    c->last_lists[1] = lists4[1];
+    c->last_lists[2] = lists4[2];
     dfree(fbl);
     dfree(fbu);
     if (e == hipSuccess) e = launch_scatter_corr(nullptr, pos, c->pts, di, d, dd, n, c->stream);

@@ -56,8 +56,8 @@ struct NNLaunch {
   int32_t* fb_list;         // queries sent to the exact reference-order DFS
   int32_t* fb_list2;        // queries a wave did not take -> ball search
   double* fb_u2;            // the distance guess u of each fb_list2 entry
-  int32_t* fb_list3;        // queries left to the per-lane certified search
-  unsigned int* fb_count;   // [0] exact, [1] ball, [2] per-lane list sizes; zero at the launch
+  unsigned int* fb_count;   // [0] exact list, [1] ball list sizes; [2] per-lane searches, [3] DFS
+                            // finishes of the ball search (counts); zero at the launch
   hipEvent_t ev_start;      // optional: the main search kernel's start and end, recorded by its
   hipEvent_t ev_fast_done;  // own dispatch (hipExtLaunchKernel: no marker packets between kernels)
   int have_prev;            // dist_out holds the previous residuals of these queries

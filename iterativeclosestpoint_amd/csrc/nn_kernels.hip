@@ -9,8 +9,9 @@
 //  k_nn_wave   the product search: 64 spatially coherent queries per wave share one search box,
 //              one cooperative walk of the octree, one lockstep fp32 filter scan, and a rigorous
 //              per-query certificate (nn_device.h) that the reference returns the same point.
-//  k_nn_ball   the queries a wave did not take, four per wave (16-lane groups), sphere walks.
-//  k_nn_lists  the rest: per-lane certified search, else the reference-order DFS.
+//  k_nn_ball   the queries a wave did not take, four per wave (16-lane groups), sphere walks; what
+//              those cannot decide, and the wave search's exact list: per-lane certified search,
+//              else the reference-order DFS.
 //
 // Everything is fp64 except the scan's filter, whose result is re-evaluated in fp64; built with
 // -ffp-contract=off (the reference is built without FMA).
@@ -849,8 +850,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
 // every leaf whose box distance s <= u (1 + 2^-47) (a sphere test) and scans their points one per
 // lane. Leaves with s > u (1 + 2^-47) only hold points with fl(d2) > best (1 + 2^-48) (monotone
 // rounding), so nothing in the certificate window is missed. Certification as in the wave search
-// (best <= u and the window test). No usable guess or an overflowing candidate set -> the lane
-// list.
+// (best <= u and the window test). A query the group cannot decide (no usable guess, an
+// overflowing candidate set, or no certificate) is finished right there by the group's first lane:
+// the per-lane certified search, else the reference-order DFS (stack in the group's LDS).
+// Before that, the kernel's threads take the exact list the wave search left, one query each
+// (the reference-order DFS). One launch for all the follow-up searches.
 constexpr int kBallGroups = 4;
 constexpr int kBallGL = 64 / kBallGroups;  // lanes per query
 constexpr int kBallStack = 512;
@@ -859,15 +863,51 @@ constexpr int kBallGStack = kBallStack / kBallGroups;
 constexpr int kBallGPoints = kBallPoints / kBallGroups;
 constexpr int kBallLdsBytes = kBallStack * 4 + kBallPoints * 4;
 
+// The reference-order DFS for query i (octree.cpp:128-184), its result written.
+__device__ __forceinline__ void exact_query(const NNLaunch& a, int64_t i, unsigned long long* st, int bs) {
+  const double qx = a.x[i], qy = a.y[i], qz = a.z[i];
+  double best_d2 = a.init_best, visits = 0.0, scanned = 0.0;
+  int32_t best = -1;
+  exact_dfs<false>(a, qx, qy, qz, st, bs, best, best_d2, visits, scanned);
+  a.pos_out[i] = best >= 0 ? best : a.pos0;
+  a.dist_out[i] = best >= 0 ? __builtin_sqrt(best_d2) : residual_to(a.pts, a.pos0, qx, qy, qz);
+}
+
+// The per-lane certified search for query i; a query it cannot certify gets the reference-order
+// DFS right away.
+__device__ __forceinline__ void lane_query(const NNLaunch& a, int64_t i, unsigned long long* st, int bs) {
+  const double qx = a.x[i], qy = a.y[i], qz = a.z[i];
+  double best = __builtin_inf(), second = __builtin_inf();
+  int32_t bpos = -1;
+  fast_dfs(a, qx, qy, qz, st, bs, best, second, bpos);
+  if (certified(best, second, a.init_best)) {
+    a.pos_out[i] = bpos;
+    a.dist_out[i] = __builtin_sqrt(best);
+  } else {
+    exact_query(a, i, st, bs);
+  }
+}
+
 __global__ void __launch_bounds__(64) k_nn_ball(NNLaunch a) {
   extern __shared__ __attribute__((aligned(16))) unsigned long long lds_raw[];
   const int lane = threadIdx.x, g = lane / kBallGL, gl = lane % kBallGL, gbase = g * kBallGL;
   int32_t* stack = reinterpret_cast<int32_t*>(lds_raw) + g * kBallGStack;
   int32_t* plist = reinterpret_cast<int32_t*>(lds_raw) + kBallStack + g * kBallGPoints;
+  // The exact list (queries the wave search could not certify): complete when this kernel starts,
+  // one thread each, a DFS stack of `levels` entries per thread in LDS.
+  {
+    const unsigned n0 = a.fb_count[0];
+    for (unsigned j = blockIdx.x * 64u + (unsigned)lane; j < n0; j += gridDim.x * 64u)
+      exact_query(a, a.fb_list[j], lds_raw + lane, 64);
+    wave_lds_fence();
+  }
+  // a group's own DFS stack (its first lane's): the group's candidate area, after its scan
+  unsigned long long* gstack = reinterpret_cast<unsigned long long*>(plist);
   const unsigned cnt = a.fb_count[1];
   for (unsigned j0 = blockIdx.x * kBallGroups; j0 < cnt; j0 += gridDim.x * kBallGroups) {
     const unsigned j = j0 + g;
     bool live = j < cnt;  // group-uniform
+    int follow = 0;       // group-uniform: 1 the per-lane search, 2 the reference-order DFS
     int64_t i = 0;
     double u = 0.0, qx = 0.0, qy = 0.0, qz = 0.0;
     if (live) {
@@ -877,7 +917,7 @@ __global__ void __launch_bounds__(64) k_nn_ball(NNLaunch a) {
       qy = a.y[i];
       qz = a.z[i];
       if (!(u <= 0x1p900)) {
-        if (gl == 0) a.fb_list3[atomicAdd(a.fb_count + 2, 1u)] = (int32_t)i;
+        follow = 1;
         live = false;
       }
     }
@@ -946,7 +986,7 @@ __global__ void __launch_bounds__(64) k_nn_ball(NNLaunch a) {
       atomicAdd(&a.dbg[14], overflow ? 1ull : 0ull);
       atomicAdd(&a.dbg[15], (unsigned long long)npts);
     }
-    if (live && overflow && gl == 0) a.fb_list3[atomicAdd(a.fb_count + 2, 1u)] = (int32_t)i;
+    if (live && overflow) follow = 1;
     if (overflow) live = false;
     wave_lds_fence();
     double best = __builtin_inf(), second = __builtin_inf();
@@ -979,46 +1019,25 @@ __global__ void __launch_bounds__(64) k_nn_ball(NNLaunch a) {
       bpos = (ob < best || (ob == best && op < bpos)) ? op : bpos;
       best = lo_;
     }
-    if (live && gl == 0) {
+    if (live) {
       if (!(best <= u)) {
-        a.fb_list3[atomicAdd(a.fb_count + 2, 1u)] = (int32_t)i;
+        follow = 1;
       } else if (certified(best, second, a.init_best)) {
-        a.pos_out[i] = bpos;
-        a.dist_out[i] = __builtin_sqrt(best);
+        if (gl == 0) {
+          a.pos_out[i] = bpos;
+          a.dist_out[i] = __builtin_sqrt(best);
+        }
       } else {
-        a.fb_list[atomicAdd(a.fb_count, 1u)] = (int32_t)i;
+        follow = 2;
       }
+    }
+    wave_lds_fence();  // the group's candidate area is free: its first lane's DFS stack
+    if (follow != 0 && gl == 0) {
+      atomicAdd(a.fb_count + (follow == 1 ? 2 : 3), 1u);  // counted for the iteration record
+      if (follow == 1) lane_query(a, i, gstack, 1);
+      else exact_query(a, i, gstack, 1);
     }
     wave_lds_fence();
-  }
-}
-
-// The two short lists the ball search leaves, in one launch: thread j < n3 takes lane-list entry
-// j (per-lane certified search; a query it cannot certify gets the reference-order DFS right
-// away, in the same thread), the rest take the exact list (queries the wave or the ball search
-// could not certify). Both lists are complete when this kernel starts; it appends nothing.
-__global__ void __launch_bounds__(64) k_nn_lists(NNLaunch a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned long long lds_stack[];
-  const unsigned n3 = a.fb_count[2], n0 = a.fb_count[0];
-  for (unsigned j = blockIdx.x * blockDim.x + threadIdx.x; j < n3 + n0; j += gridDim.x * blockDim.x) {
-    const bool lane_list = j < n3;
-    const int64_t i = lane_list ? a.fb_list3[j] : a.fb_list[j - n3];
-    const double qx = a.x[i], qy = a.y[i], qz = a.z[i];
-    if (lane_list) {
-      double best = __builtin_inf(), second = __builtin_inf();
-      int32_t bpos = -1;
-      fast_dfs(a, qx, qy, qz, lds_stack + threadIdx.x, blockDim.x, best, second, bpos);
-      if (certified(best, second, a.init_best)) {
-        a.pos_out[i] = bpos;
-        a.dist_out[i] = __builtin_sqrt(best);
-        continue;
-      }
-    }
-    double best_d2 = a.init_best, visits = 0.0, scanned = 0.0;
-    int32_t best = -1;
-    exact_dfs<false>(a, qx, qy, qz, lds_stack + threadIdx.x, blockDim.x, best, best_d2, visits, scanned);
-    a.pos_out[i] = best >= 0 ? best : a.pos0;
-    a.dist_out[i] = best >= 0 ? __builtin_sqrt(best_d2) : residual_to(a.pts, a.pos0, qx, qy, qz);
   }
 }
 
@@ -1068,14 +1087,15 @@ hipError_t launch_nn(const NNLaunch& a, hipStream_t s) {
     case 4: wave(k_nn_wave<false, 4>); break;
     default: return hipErrorInvalidValue;
   }
-  // the lists are short (usually empty after the first iteration): small grids of 64-thread
-  // blocks, grid-stride over the list
+  // the follow-up lists are short (the ball list ~0.1 % of the queries, the exact list usually
+  // empty): one launch of 64-thread blocks, grid-stride over them; LDS for the group stacks and
+  // lists or, before them, one DFS stack of `levels` entries per thread
   const int64_t bq = (a.n + kBallGroups - 1) / kBallGroups;
-  hipLaunchKernelGGL(k_nn_ball, dim3((unsigned)(bq < 8192 ? bq : 8192)), dim3(64), kBallLdsBytes, s, a);
-  const int64_t lq = (a.n + 63) / 64;
-  size_t lshm = (size_t)levels * 64 * sizeof(unsigned long long);
-  if (lshm < 1024) lshm = 1024;
-  hipLaunchKernelGGL(k_nn_lists, dim3((unsigned)(lq < 1024 ? lq : 1024)), dim3(64), lshm, s, a);
+  size_t bshm = (size_t)levels * 64 * sizeof(unsigned long long);
+  if (bshm < (size_t)kBallLdsBytes) bshm = kBallLdsBytes;
+  static_assert(kBallGPoints * 4 >= 64 * 8, "a group's DFS stack (stride 1) holds >= 64 levels");
+  if (levels > kBallGPoints * 4 / 8) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_nn_ball, dim3((unsigned)(bq < 8192 ? bq : 8192)), dim3(64), bshm, s, a);
   return hipGetLastError();
 }
 

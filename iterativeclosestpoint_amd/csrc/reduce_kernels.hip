@@ -225,10 +225,11 @@ __device__ void finalize_cov_publish(IterDev* it, const CovMoments& g, IterPubli
   if (threadIdx.x == 0) {
     rec->c_global = g;
     rec->rmse = (g.n > 0) ? __builtin_sqrt(g.sum_d2 / g.n) : 0.0;  // icpengine.cpp:274-278
-    for (int k = 0; k < 3; k++) {
-      rec->pad[k] = (double)pub.lists[k];
-      pub.lists[k] = 0u;
-    }
+    // exact (the wave search's list + the ball search's DFS finishes), ball, per-lane
+    rec->pad[0] = (double)(pub.lists[0] + pub.lists[3]);
+    rec->pad[1] = (double)pub.lists[1];
+    rec->pad[2] = (double)pub.lists[2];
+    for (int k = 0; k < 4; k++) pub.lists[k] = 0u;
     it->c_global = rec->c_global;
     it->rmse = rec->rmse;
   }
