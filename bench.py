@@ -4,6 +4,8 @@
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--points 10000000]
     torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU)
+    python bench.py --gpus N ...   (N > 1 without a launcher: one process drives the N GPUs,
+                                    icp_hip_create_multi; the drop-in's single-process path)
 
 A step = one full ICP iteration of the product engine (icp_session_step): fused transform of
 the resident source + exact octree NN + residual + 3-sigma statistics (RCCL all-gather) + cull
@@ -25,6 +27,12 @@ iterations (max over ranks); `median` = the same rate from the median iteration 
                 1 thread, on a bounded sample of the same workload (rank 0, N=1 only).
   cpu_allcores  the CPU restatement (oracle/icp_oracle.c, OpenMP NN loop) on every core of this
                 process's CPU set, full size, from the parity leg below.
+  timed_state_parity  (N=1) the correspondences and residuals of the LAST TIMED iterate (the
+                candidate-cache state the figure was measured in) against the CPU oracle's octree
+                NN on the same moved source, every query: mismatch counts (bit for bit).
+  registration  (N=1) a registration of the full clouds with the reference's stops on
+                (ICPParameters defaults): iterations taken, wall, mean Mcorr/s over all iterates
+                including the first, the first iterate's share.
   parity        (N=1) a fresh engine registration of the full clouds for --parity-iters
                 iterations on the GPU and on the CPU oracle: final transform RMSE (north star:
                 <= 1e-6), per-iteration valid counts, final RMSE.
@@ -139,6 +147,44 @@ def cpu_baseline(tgt: np.ndarray, src: np.ndarray, sample: int) -> dict | None:
             "sample": f"{len(pick)} of {len(src)} queries vs full target, oracle/icp_oracle.c, CPU {cpu_model()}"}
 
 
+def timed_state_parity(tgt: np.ndarray, q: np.ndarray, idx: np.ndarray, d: np.ndarray, iterate: int) -> dict:
+    """The correspondences and residuals of the LAST TIMED iterate (candidate cache state and all)
+    against the CPU oracle's octree NN on the same moved source, every query (OpenMP)."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import oracle_py  # test infrastructure: the checker only
+
+    cores = cpu_threads()
+    oracle_py.set_threads(cores)
+    t0 = time.perf_counter()
+    oidx, od = oracle_py.OracleTree(tgt).nn(q, init_best=oracle_py.DBL_MAX)
+    return {"iterate": iterate, "checked": int(len(q)),
+            "idx_mismatch": int(np.count_nonzero(idx != oidx)),
+            "dist_mismatch": int(np.count_nonzero(d.view(np.uint64) != od.view(np.uint64))),
+            "checker": f"oracle/icp_oracle.c octree NN (octree.cpp:128-184), {cores} threads, "
+                       f"{time.perf_counter() - t0:.1f} s"}
+
+
+def registration_leg(icp, ctx, src: np.ndarray) -> dict:
+    """A real registration of the full clouds with the reference's stops on (ICPParameters defaults:
+    50 iterations, tolerance 1e-6, 3x no improvement, divergence; icpengine.cpp:287-323): what one
+    registration costs end to end on the resident target, first iterate included."""
+    ctx.set_source(src)
+    p = icp.params_default()
+    sess = ctx.session(p)
+    ms = sess.step_n_timed(p.max_iterations + 1)
+    rc, res = sess.finish()
+    sess.close()
+    n = len(src)
+    total = float(np.sum(ms))
+    status = {0: "max_iterations", 1: "converged", 2: "diverged", 3: "too_few", 4: "cancelled"}.get(res.status, "?")
+    return {"iterations": len(ms), "status": status, "wall_ms": round(total, 3),
+            "mean_value": round(n * len(ms) / total / 1e3, 3), "unit": "Mcorr/s",
+            "first_iteration_ms": round(float(ms[0]), 4), "first_iteration_share": round(float(ms[0]) / total, 4),
+            "final_rmse": res.final_rmse,
+            "note": "ICPParameters defaults (icpengine.h:13-19) with the reference's stops on; wall = sum of "
+                    "the steps (set_source excluded); mean_value = n x iterations / wall"}
+
+
 def parity_leg(icp, ctx, tgt: np.ndarray, src: np.ndarray, iters: int) -> tuple[dict, dict]:
     """A fresh engine registration (tolerance 0: exactly `iters` iterations) of the full clouds on
     the GPU and on the CPU oracle (OpenMP over all cores of this process). Returns the parity
@@ -218,7 +264,9 @@ def main() -> int:
     ap.add_argument("--cpu-sample", type=int, default=1_000_000)
     ap.add_argument("--parity-iters", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--no-parity", action="store_true",
+                    help="skip the CPU checks (the timed state's correspondences and the fresh registration)")
+    ap.add_argument("--no-registration", action="store_true", help="skip the stops-on registration leg")
     ap.add_argument("--exchange", choices=("rccl", "host"), default="rccl",
                     help="per-iteration all-gathers: RCCL (default), or over torch.distributed gloo "
                          "through the host (rehearsal of N ranks on one GPU; RCCL refuses that)")
@@ -252,8 +300,13 @@ def main() -> int:
             dist.barrier()
     n_dev = max(1, torch.cuda.device_count())
     device = local_rank % n_dev  # ranks > GPUs only in host-exchange rehearsals
-    gpus_used = min(world, n_dev)
-    shared_gpu = world > gpus_used
+    # --gpus N > 1 without a launcher: one process drives all N devices (icp_hip_create_multi:
+    # a driver thread per device, RCCL from ncclCommInitAll; devices repeat only in a rehearsal on
+    # fewer GPUs, which then uses the in-process host gather)
+    group = world == 1 and args.gpus > 1
+    shards = args.gpus if group else world
+    gpus_used = min(shards, n_dev)
+    shared_gpu = shards > gpus_used
     torch.cuda.set_device(device)
 
     n = args.points
@@ -269,7 +322,7 @@ def main() -> int:
     if args.config:
         kv = dict(c.split("=", 1) for c in args.config)
         conf = icp.config(**{k: (float(v) if "." in v else int(v)) for k, v in kv.items()})
-    ctx = icp.Context(device, conf)
+    ctx = icp.Context(devices=[k % n_dev for k in range(args.gpus)], cfg=conf) if group else icp.Context(device, conf)
     ctx.set_target(tgt, 10, 20, icp.RULES_ENGINE)
     # spatial shards: contiguous ranges of the kd order (a contiguous range of the shuffled cloud
     # would thin each rank's queries `world` times; see icp_host.h icp_source_shard_order)
@@ -320,6 +373,12 @@ def main() -> int:
         elapsed, med_ms = float(t[0].item()), float(t[1].item())
     # HIP events of the timed iterates (read after the timed region)
     nn_ms, it_ms = ctx.timings(min(args.steps, 256))
+    # untimed: the state the last timed iterate left (its queries = the moved source, and its
+    # correspondences/residuals), checked against the CPU oracle below
+    timed_q = timed_idx = timed_d = None
+    if rank == 0 and world == 1 and not args.no_parity:
+        timed_q = ctx.get_source()
+        timed_idx, timed_d = ctx.get_correspondences()
     # untimed: how the last timed state splits over the search paths (same queries, same guess)
     probe = ctx.iterate(None, 1, icp.RULES_ENGINE, 3.0)
     rc, res = sess.finish()
@@ -328,7 +387,7 @@ def main() -> int:
     v_mean, p_mean = ctx.traversal_counts() if rank == 0 else (None, None)
 
     info = ctx.target_info()
-    n_local = hi - lo
+    n_local = n // shards if group else hi - lo  # per device
     nn_avg_s = float(np.mean(nn_ms)) / 1e3
     need = compulsory_bytes(n_local, n, n, info["n_nodes"])
     achieved = need / nn_avg_s / 1e9
@@ -338,7 +397,7 @@ def main() -> int:
         try:
             tr = json.loads(tj.read_text())
             # only a profile of this exact kernel source and workload counts
-            if tr.get("n") == n and tr.get("world") == world and tr.get("search_src_sha1") == search_source_sha1():
+            if tr.get("n") == n and tr.get("world") == shards and tr.get("search_src_sha1") == search_source_sha1():
                 traffic = tr.get("bytes_per_launch")
         except Exception:
             traffic = None
@@ -351,6 +410,19 @@ def main() -> int:
             cpu = cpu_baseline(tgt, src, args.cpu_sample)
         except Exception as e:  # keep the bench line even if the baseline cannot run
             cpu = {"value": None, "unit": "Mcorr/s", "cores": 1, "kind": "reference", "sample": f"failed: {e}"}
+    timed_parity = None
+    if timed_q is not None:
+        try:
+            timed_parity = timed_state_parity(tgt, timed_q, timed_idx, timed_d, args.warmup + args.steps)
+        except Exception as e:
+            timed_parity = {"error": str(e)}
+        del timed_q, timed_idx, timed_d
+    registration = None
+    if rank == 0 and world == 1 and not args.no_registration:
+        try:
+            registration = registration_leg(icp, ctx, src)
+        except Exception as e:
+            registration = {"error": str(e)}
     if rank == 0 and world == 1 and not args.no_parity and args.parity_iters > 0:
         try:
             parity, allcores = parity_leg(icp, ctx, tgt, src, args.parity_iters)
@@ -358,7 +430,7 @@ def main() -> int:
             parity = {"error": str(e)}
 
     if rank == 0:
-        nq = max(1, n_local)
+        nq = max(1, n_local * (shards if group else 1))
         line = {
             "metric": METRIC,
             "value": round(value, 3),
@@ -378,10 +450,13 @@ def main() -> int:
             "config": {
                 "workload": f"{CONFIG_NAMES.get(n, 'custom')}: {n}<->{n} synthetic pair, full ICP iteration "
                             f"(engine rules, octree leaf 10 / depth 20), "
-                            f"source sharded over {world} rank(s) on {gpus_used} GPU(s), target octree replicated",
-                "n_target": n, "n_source": n, "ranks": world, "ranks_per_gpu": world // gpus_used,
-                "parallelism": f"spatial source shards x{world} (kd-order ranges; "
-                + ("RCCL" if args.exchange == "rccl" else "host/gloo rehearsal") + " all-gather of 2 moment records per iteration)"
+                            f"source sharded over {shards} rank(s) on {gpus_used} GPU(s), target octree replicated",
+                "n_target": n, "n_source": n, "ranks": shards, "ranks_per_gpu": shards // gpus_used,
+                "parallelism": f"spatial source shards x{shards} (kd-order ranges; "
+                + (("one process, a driver thread per device, " + ("RCCL (ncclCommInitAll)" if not shared_gpu else
+                                                                   "in-process host gather rehearsal"))
+                   if group else ("RCCL" if args.exchange == "rccl" else "host/gloo rehearsal"))
+                + " all-gather of 2 moment records per iteration)"
                 + ("; 1-rank RCCL communicator (multi-rank path)" if world == 1 and args.rccl_self else ""),
                 "octree_nodes": info["n_nodes"], "octree_leaves": info["n_leaves"],
             },
@@ -403,7 +478,8 @@ def main() -> int:
                 "iterate_device_ms_avg": round(float(np.mean(it_ms)), 4),
                 "model": f"{STREAM_B_PER_QUERY} B/query streamed + {TGT_B_PER_POINT} B/target point + {NODE_B} B/node, each once",
             },
-            "search_paths": {"queries": n_local, "wave": n_local - int(probe.n_ball_search),
+            "search_paths": {"queries": n_local * (shards if group else 1),
+                             "wave": n_local * (shards if group else 1) - int(probe.n_ball_search),
                              "ball": int(probe.n_ball_search), "lane": int(probe.n_lane_search),
                              "exact_fallback": int(probe.n_fallback),
                              "ball_share": round(probe.n_ball_search / nq, 6),
@@ -415,6 +491,8 @@ def main() -> int:
             "cpu_baseline": cpu,
             "cpu_allcores": allcores,
             "parity": parity,
+            "timed_state_parity": timed_parity,
+            "registration": registration,
             "setup_s": round(setup_s, 2),
             "octree_build": {"on_device": build_on_dev, "ms": round(build_ms, 2)},
             "final_rmse": res.final_rmse,

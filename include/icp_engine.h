@@ -9,10 +9,12 @@
  *   icp_engine_register       ICPEngine::setParameters + registerPointClouds (+ stop via the
  *                             stop flag, signals via hooks)   core/icpengine.h:60-75,
  *                             icpengine.cpp:24-66, :117-394
+ *   icp_engine_register_devices  the same over several GPUs of one process
  *   icp_engine_run            the same loop on an existing (possibly multi-GPU) context
  *   icp_cli_icp               void ICP(PointCloud&, const PointCloud&, int, double,
  *                             double[3][3], double[3], vector<Matrix4d>*)
  *                             icp_registration.cpp:443-622
+ *   icp_cli_icp_devices       the same over several GPUs of one process
  *   icp_best_fit_transform    computeBestFitTransform / best_fit_transform
  *                             icpengine.cpp:76-115, icp_registration.cpp:389-440 (host)
  *   icp_jacobi_svd3           Eigen::JacobiSVD<Matrix3d> as used at icpengine.cpp:93 (host)
@@ -94,6 +96,13 @@ int icp_engine_register(const icp_params* p, double* src_xyz, int64_t n_src, con
                         int64_t n_tgt, int device, icp_result* res, icp_iteration_record* history,
                         int32_t history_cap, const icp_engine_hooks* hooks);
 
+/* The same on several GPUs of this process (icp_hip_create_multi: the source sharded over the
+ * devices, the octree replicated, RCCL all-gathers of the two per-iteration records when the ids
+ * are distinct, an in-process host gather when they repeat). n_devices = 1 is icp_engine_register. */
+int icp_engine_register_devices(const icp_params* p, double* src_xyz, int64_t n_src, const double* tgt_xyz,
+                                int64_t n_tgt, int n_devices, const int* device_ids, icp_result* res,
+                                icp_iteration_record* history, int32_t history_cap, const icp_engine_hooks* hooks);
+
 /* The loop on a context that already holds target + this rank's source shard (icp_hip.h).
  * Every rank of a communicator calls it in lockstep; decisions are identical on all ranks.
  * The resident source is left transformed; fetch it with icp_hip_get_source. */
@@ -124,6 +133,11 @@ void icp_session_destroy(icp_session* s);
 int icp_cli_icp(double* src_xyz, int64_t n_src, const double* tgt_xyz, int64_t n_tgt, int max_iterations,
                 double tolerance, double final_R[9], double final_t[3], double* iteration_transforms,
                 int32_t cap, int32_t* n_transforms, int device);
+
+/* icp_cli_icp on several GPUs of this process (as icp_engine_register_devices). */
+int icp_cli_icp_devices(double* src_xyz, int64_t n_src, const double* tgt_xyz, int64_t n_tgt, int max_iterations,
+                        double tolerance, double final_R[9], double final_t[3], double* iteration_transforms,
+                        int32_t cap, int32_t* n_transforms, int n_devices, const int* device_ids);
 
 /* Host helpers (no GPU needed). */
 void icp_jacobi_svd3(const double H[9], double U[9], double S[3], double V[9]);

@@ -48,6 +48,9 @@ struct ICPParameters {
   int octreeMaxPoints = 10;
   int octreeMaxDepth = 20;
   int device = -1;  // build-only knob: HIP ordinal (-1: the calling thread's current device)
+  // build-only knob: several GPUs of this process (the source sharded over them, the octree
+  // replicated, RCCL per iteration); empty = `device` alone
+  std::vector<int> devices;
 };
 
 struct IterationResult {
@@ -107,9 +110,11 @@ class ICPEngine {
     hooks.on_log = &ICPEngine::logThunk;
     hooks.stop_flag = reinterpret_cast<const volatile int32_t*>(&stop_);
     icp_result r;
-    int rc = icp_engine_register(&p, reinterpret_cast<double*>(source->points.data()), (int64_t)source->size(),
-                                 reinterpret_cast<const double*>(target->points.data()), (int64_t)target->size(),
-                                 params_.device, &r, hist.data(), (int32_t)hist.size(), &hooks);
+    std::vector<int> devs = params_.devices.empty() ? std::vector<int>{params_.device} : params_.devices;
+    int rc = icp_engine_register_devices(&p, reinterpret_cast<double*>(source->points.data()), (int64_t)source->size(),
+                                         reinterpret_cast<const double*>(target->points.data()),
+                                         (int64_t)target->size(), (int)devs.size(), devs.data(), &r, hist.data(),
+                                         (int32_t)hist.size(), &hooks);
     for (int k = 0; k < r.n_history; k++) result_.iterationHistory.push_back(convert(hist[k]));
     if (rc != ICP_HIP_OK) return finish(false, r.message);
     result_.success = true;
@@ -203,14 +208,15 @@ class Octree {
 // (icp_registration.cpp:443-446); Matrix4d replaced by a row-major 4x4 array.
 using Matrix4 = std::array<double, 16>;
 inline void ICP(PointCloud& source, const PointCloud& target, int max_iterations, double tolerance,
-                double final_R[3][3], double final_t[3], std::vector<Matrix4>* iteration_transforms = nullptr,
-                int device = -1) {
+                double final_R[3][3], double final_t[3], std::vector<Matrix4>* iteration_transforms,
+                const std::vector<int>& devices) {
   std::vector<double> tr((size_t)(max_iterations > 0 ? max_iterations : 1) * 16);
   int32_t n = 0;
   double R[9], t[3];
-  int rc = icp_cli_icp(reinterpret_cast<double*>(source.points.data()), (int64_t)source.size(),
-                       reinterpret_cast<const double*>(target.points.data()), (int64_t)target.size(), max_iterations,
-                       tolerance, R, t, tr.data(), (int32_t)(tr.size() / 16), &n, device);
+  int rc = icp_cli_icp_devices(reinterpret_cast<double*>(source.points.data()), (int64_t)source.size(),
+                               reinterpret_cast<const double*>(target.points.data()), (int64_t)target.size(),
+                               max_iterations, tolerance, R, t, tr.data(), (int32_t)(tr.size() / 16), &n,
+                               (int)devices.size(), devices.data());
   if (rc != ICP_HIP_OK) throw std::runtime_error(icp_hip_last_error());
   for (int i = 0; i < 3; i++) {
     for (int j = 0; j < 3; j++) final_R[i][j] = R[3 * i + j];
@@ -222,6 +228,11 @@ inline void ICP(PointCloud& source, const PointCloud& target, int max_iterations
       for (int e = 0; e < 16; e++) m[e] = tr[16 * k + e];
       iteration_transforms->push_back(m);
     }
+}
+inline void ICP(PointCloud& source, const PointCloud& target, int max_iterations, double tolerance,
+                double final_R[3][3], double final_t[3], std::vector<Matrix4>* iteration_transforms = nullptr,
+                int device = -1) {
+  ICP(source, target, max_iterations, tolerance, final_R, final_t, iteration_transforms, std::vector<int>{device});
 }
 
 }  // namespace icp_amd

@@ -77,7 +77,14 @@ typedef struct icp_hip_config {
                                (an exact containment test: results are unchanged); 0: every
                                iterate walks                                              dflt 1 */
   int32_t candidate_margin; /* see candidate_cache, in [0, 1024]                        dflt 16 */
-  int32_t reserved[3];    /* zero */
+  int32_t certify_prev;   /* after an iterate on the same queries, a query whose previous match p*
+                             is certified by p*'s separation (a lower bound of p*'s distance to
+                             every other target point, computed once per target) keeps it without
+                             a search (exact: the window certificate of DESIGN.md §3.1).
+                             0: off; 1: only waves whose every query is certified skip the search;
+                             2: certified queries settle, the rest of the wave searches;
+                             3: certified queries settle, the rest take the ball search   dflt 0 */
+  int32_t reserved[2];    /* zero */
 } icp_hip_config;
 
 /* Slots of icp_hip_debug_counters (summed over the last iterate's search launches). */
@@ -97,12 +104,19 @@ typedef struct icp_hip_config {
 #define ICP_DBG_CACHE_STORES 13  /* waves that walked and stored their candidate list          */
 #define ICP_DBG_BALL_OVERFLOW 14 /* ball-search queries whose candidate set overflowed         */
 #define ICP_DBG_BALL_POINTS 15   /* points scanned by the ball search                          */
-#define ICP_DBG_CLK_GUESS 16     /* wave clocks (s_memtime): guess + box                       */
-#define ICP_DBG_CLK_WALK 17      /*                          walk                              */
-#define ICP_DBG_CLK_SCAN 18      /*                          scan                              */
-#define ICP_DBG_CLK_FINISH 19    /*                          certify + write + queue           */
-#define ICP_DBG_CLK_START 20     /*                          start nodes (cells or descent)    */
+#define ICP_DBG_CLK_GUESS 16     /* phase-clock build (-DICP_PHASE_CLOCKS=1), s_memtime: guess  */
+#define ICP_DBG_CLK_BOX 17       /*                          search box                        */
+#define ICP_DBG_CLK_WALK 18      /*                          walk (cells + batches)            */
+#define ICP_DBG_CLK_SCAN 19      /*                          scan                              */
+#define ICP_DBG_PREV_WAVES 18    /* count build: waves whose every query the previous-match
+                                    certificate settled (certify_prev)                           */
+#define ICP_DBG_PREV_LANES 19    /* count build: queries settled by the previous-match certificate */
+#define ICP_DBG_CLK_FINISH 20    /*                          certify + write + queue           */
+#define ICP_DBG_WINNER_PREV_WAVES 20 /* winner-count build (-DICP_WINNER_COUNTS=1): waves whose
+                                        every fp32 winner is the lane's previous match          */
 #define ICP_DBG_START_NODES 21   /* start nodes taken from the cell tables / descent levels    */
+#define ICP_DBG_WINNER_PREV 22   /* winner-count build: joined lanes whose winner is the previous match */
+#define ICP_DBG_WINNER_LANES 23  /* winner-count build: joined lanes with an fp32 winner          */
 #define ICP_DBG_SLOTS 24
 
 typedef struct icp_hip_ctx icp_hip_ctx;
@@ -139,6 +153,29 @@ int icp_hip_create(icp_hip_ctx** out, int device);
 int icp_hip_create_ex(icp_hip_ctx** out, int device, const icp_hip_config* cfg);
 void icp_hip_destroy(icp_hip_ctx* ctx);
 
+/* Transports of a multi-device context (icp_hip_create_multi); icp_hip_ctx_devices also reports
+ * ICP_XPORT_CALLBACK (icp_hip_comm_init_host) and ICP_XPORT_AUTO (= none: a world of one). */
+#define ICP_XPORT_AUTO 0     /* RCCL when the device ids are distinct, else the host gather       */
+#define ICP_XPORT_RCCL 1     /* communicators from ncclCommInitAll (distinct devices)            */
+#define ICP_XPORT_HOST 2     /* in-process host gather (any ids: rehearses N ranks on one GPU)   */
+#define ICP_XPORT_CALLBACK 3 /* the caller's exchange callback (icp_hip_comm_init_host)          */
+
+/* One context driving n_devices GPUs from this process: the multi-GPU path behind the
+ * single-process drop-in (ICPEngine::registerPointClouds, icpengine.cpp:24-60; CLI ICP(),
+ * icp_registration.cpp:443-446; SURVEY.md §8b icp_hip_create(ctx, n_devices, device_ids)).
+ * The source is sharded over the devices in spatially compact ranges (icp_source_shard_order),
+ * the octree replicated; each device has a driver thread of its own, and the two per-iteration
+ * exchanges are RCCL all-gathers over communicators from ncclCommInitAll (ICP_XPORT_RCCL) or an
+ * in-process host gather (ICP_XPORT_HOST). Every other entry point of this header accepts the
+ * returned context as it accepts a single-device one: outputs in the caller's order, statistics
+ * identical on all devices (those of a world of n_devices processes), timings the slowest
+ * device's, search-path counts summed. comm_init / comm_init_host do not apply to it. A source
+ * needs at least one point per device. n_devices = 1 with ICP_XPORT_AUTO gives a plain context. */
+int icp_hip_create_multi(icp_hip_ctx** out, int n_devices, const int* device_ids, const icp_hip_config* cfg,
+                         int transport);
+/* Devices (up to cap ids) and transport (ICP_XPORT_*) of a context. */
+int icp_hip_ctx_devices(icp_hip_ctx* ctx, int32_t* n_devices, int32_t* device_ids, int32_t cap, int32_t* transport);
+
 /* Multi-GPU: rank 0 calls get_unique_id, the caller distributes the bytes (any side channel),
  * then every rank calls comm_init. Without it a context is a world of one. A communicator of
  * one rank (nranks = 1) is created as well: every iteration then runs the multi-rank path
@@ -153,7 +190,10 @@ int icp_hip_comm_init(icp_hip_ctx* ctx, int nranks, int rank, const uint8_t id[I
  * rehearse several ranks on one GPU (RCCL refuses two ranks on one device) and by callers that
  * already own a host transport. Slower than RCCL: the stream is synchronised around each call.
  * A failing callback makes icp_hip_iterate return ICP_HIP_EEXCHANGE; the peer ranks are then
- * left waiting inside their own exchange, and the caller must tear them down. */
+ * left waiting inside their own exchange, and the caller must tear them down.
+ * When icp_hip_iterate fails with ICP_HIP_EEXCHANGE or ICP_HIP_ERCCL, its T_apply has ALREADY
+ * been applied to the resident source (the search kernel moves the queries before the exchange):
+ * a caller that retries the iterate must pass T_apply = null. */
 typedef int (*icp_hip_exchange_fn)(void* user, const double* local, int32_t count, double* gathered);
 int icp_hip_comm_init_host(icp_hip_ctx* ctx, int nranks, int rank, icp_hip_exchange_fn exchange, void* user);
 
@@ -172,6 +212,11 @@ int icp_hip_target_build_info(icp_hip_ctx* ctx, int32_t* on_device, double* buil
  * (icp_host.h); sizes from icp_hip_target_info (nodes) and the target size (points). */
 int icp_hip_copy_target(icp_hip_ctx* ctx, double* box6, int32_t* first, uint32_t* meta, int32_t* depth,
                         double* xyz, int32_t* orig);
+
+/* The separation of every target point (caller's target order): a lower bound of its distance
+ * to every other target point, 0 when it has an exact duplicate (computed by set_target when
+ * config certify_prev != 0; zeros otherwise). Inspection / tests. */
+int icp_hip_target_separation(icp_hip_ctx* ctx, float* sep_out);
 
 /* Upload this rank's source shard (AoS xyz). Queries are reordered on the device along a
  * Morton curve for traversal coherence; every output is returned in the caller's order. */
@@ -209,7 +254,8 @@ int icp_hip_target_info(icp_hip_ctx* ctx, int64_t* n_nodes, int64_t* n_leaves, i
  * whole device part of the last iterate. */
 int icp_hip_last_timing(icp_hip_ctx* ctx, double* nn_kernel_ms, double* iterate_device_ms);
 
-/* The same for each of the last k iterates (k <= 64), oldest first. Waits for them to finish. */
+/* The same for each of the last k iterates (k <= 256, the context's timing ring), oldest first.
+ * Waits for them to finish. */
 int icp_hip_timings(icp_hip_ctx* ctx, int k, double* nn_kernel_ms, double* iterate_device_ms);
 
 /* The wave search's diagnostic counters of the last iterate (ICP_DBG_* slots); zeros unless the

@@ -41,5 +41,9 @@ from ._lib import (  # noqa: F401
     SEARCH_REFERENCE,
     BUILD_AUTO,
     BUILD_HOST,
+    XPORT_AUTO,
+    XPORT_RCCL,
+    XPORT_HOST,
+    XPORT_CALLBACK,
     DBG_NAMES,
 )

@@ -19,13 +19,18 @@ SEARCH_CERTIFIED = 0
 SEARCH_REFERENCE = 1
 BUILD_AUTO = 0
 BUILD_HOST = 1
+XPORT_AUTO = 0
+XPORT_RCCL = 1
+XPORT_HOST = 2
+XPORT_CALLBACK = 3
 DBG_SLOTS = 24
 # icp_hip.h ICP_DBG_* slot names
 DBG_NAMES = {0: "waves", 1: "overflow_waves", 2: "not_joined", 3: "not_covered", 4: "scanned_points",
              8: "fp64_scan_waves", 9: "staged_points", 10: "scan_pairs", 11: "scan_rounds",
              12: "cache_hits", 13: "cache_stores",
              5: "walk_batches", 6: "no_guess", 7: "candidates", 14: "ball_overflow", 15: "ball_points",
-             21: "start_nodes"}
+             21: "start_nodes", 20: "winner_prev_waves", 22: "winner_prev", 23: "winner_lanes",
+             18: "prev_cert_waves", 19: "prev_cert_lanes"}
 
 _P = C.c_void_p
 _D = C.POINTER(C.c_double)
@@ -61,7 +66,7 @@ class HipConfig(C.Structure):
         ("search", C.c_int32), ("scan32", C.c_int32), ("cell_starts", C.c_int32),
         ("octree_builder", C.c_int32), ("join_factor", C.c_double), ("debug_counters", C.c_int32),
         ("xcd_blocks", C.c_int32), ("scan_groups", C.c_int32), ("candidate_cache", C.c_int32),
-        ("candidate_margin", C.c_int32), ("reserved", C.c_int32 * 3),
+        ("candidate_margin", C.c_int32), ("certify_prev", C.c_int32), ("reserved", C.c_int32 * 2),
     ]
 
 
@@ -134,6 +139,8 @@ SIGNATURES = {
     "icp_hip_config_default": (None, [C.POINTER(HipConfig)]),
     "icp_hip_create": (C.c_int, [C.POINTER(C.c_void_p), C.c_int]),
     "icp_hip_create_ex": (C.c_int, [C.POINTER(C.c_void_p), C.c_int, C.POINTER(HipConfig)]),
+    "icp_hip_create_multi": (C.c_int, [C.POINTER(C.c_void_p), C.c_int, _I32, C.POINTER(HipConfig), C.c_int]),
+    "icp_hip_ctx_devices": (C.c_int, [_P, _I32, _I32, C.c_int32, _I32]),
     "icp_hip_debug_counters": (C.c_int, [_P, _P]),
     "icp_hip_destroy": (None, [_P]),
     "icp_hip_get_unique_id": (C.c_int, [C.c_char_p]),
@@ -152,6 +159,7 @@ SIGNATURES = {
     "icp_hip_timings": (C.c_int, [_P, C.c_int, _P, _P]),
     "icp_hip_target_build_info": (C.c_int, [_P, _I32, _D]),
     "icp_hip_copy_target": (C.c_int, [_P, _P, _P, _P, _P, _P, _P]),
+    "icp_hip_target_separation": (C.c_int, [_P, _P]),
     "icp_hip_synchronize": (C.c_int, [_P]),
     "icp_hip_last_error": (C.c_char_p, []),
     # icp_engine.h
@@ -159,6 +167,9 @@ SIGNATURES = {
     "icp_engine_register": (C.c_int, [C.POINTER(Params), _P, C.c_int64, _P, C.c_int64, C.c_int,
                                       C.POINTER(Result), C.POINTER(IterationRecord), C.c_int32,
                                       C.POINTER(Hooks)]),
+    "icp_engine_register_devices": (C.c_int, [C.POINTER(Params), _P, C.c_int64, _P, C.c_int64, C.c_int, _I32,
+                                              C.POINTER(Result), C.POINTER(IterationRecord), C.c_int32,
+                                              C.POINTER(Hooks)]),
     "icp_engine_run": (C.c_int, [_P, C.POINTER(Params), C.POINTER(Result), C.POINTER(IterationRecord),
                                  C.c_int32, C.POINTER(Hooks)]),
     "icp_session_create": (C.c_int, [_P, C.POINTER(Params), C.POINTER(Hooks), C.POINTER(C.c_void_p)]),
@@ -170,6 +181,8 @@ SIGNATURES = {
     "icp_session_destroy": (None, [_P]),
     "icp_cli_icp": (C.c_int, [_P, C.c_int64, _P, C.c_int64, C.c_int, C.c_double, _P, _P, _P, C.c_int32,
                               _I32, C.c_int]),
+    "icp_cli_icp_devices": (C.c_int, [_P, C.c_int64, _P, C.c_int64, C.c_int, C.c_double, _P, _P, _P, C.c_int32,
+                                      _I32, C.c_int, _I32]),
     "icp_jacobi_svd3": (None, [_P, _P, _P, _P]),
     "icp_best_fit_transform": (None, [_P, _P, C.c_int64, _P]),
     "icp_best_fit_from_stats": (None, [C.POINTER(IterStats), _P]),
@@ -268,11 +281,16 @@ class Context:
     """One GPU context (icp_hip_ctx) — see include/icp_hip.h. `cfg` is an icp_hip_config (or a
     dict of its fields); None = the library defaults."""
 
-    def __init__(self, device: int = 0, cfg=None):
+    def __init__(self, device: int = 0, cfg=None, devices=None, transport: int = XPORT_AUTO):
+        """devices = a list of HIP ordinals: one context over all of them (icp_hip_create_multi)."""
         self._h = C.c_void_p()
         if isinstance(cfg, dict):
             cfg = config(**cfg)
-        if cfg is None:
+        if devices is not None:
+            ids = (C.c_int32 * len(devices))(*devices)
+            _check(lib().icp_hip_create_multi(C.byref(self._h), len(devices), ids,
+                                              None if cfg is None else C.byref(cfg), transport))
+        elif cfg is None:
             _check(lib().icp_hip_create(C.byref(self._h), device))
         else:
             _check(lib().icp_hip_create_ex(C.byref(self._h), device, C.byref(cfg)))
@@ -298,6 +316,13 @@ class Context:
     @property
     def handle(self):
         return self._h
+
+    def devices(self):
+        """(device ids, transport) of this context (ICP_XPORT_*)."""
+        n, tr = C.c_int32(), C.c_int32()
+        ids = (C.c_int32 * 64)()
+        _check(lib().icp_hip_ctx_devices(self._h, C.byref(n), ids, 64, C.byref(tr)))
+        return [ids[k] for k in range(n.value)], tr.value
 
     @staticmethod
     def unique_id() -> bytes:
@@ -395,6 +420,12 @@ class Context:
         return {"box": box, "first": first, "meta": meta, "depth": depth, "pts": pts, "orig": orig,
                 "n_leaves": info["n_leaves"], "max_depth": info["max_depth"]}
 
+    def target_separation(self) -> np.ndarray:
+        """Per target point (caller's order): lower bound of its distance to every other point."""
+        out = np.empty(self._n_tgt, np.float32)
+        _check(lib().icp_hip_target_separation(self._h, _ptr(out)))
+        return out
+
     def last_timing(self):
         a, b = C.c_double(), C.c_double()
         _check(lib().icp_hip_last_timing(self._h, C.byref(a), C.byref(b)))
@@ -488,7 +519,7 @@ class Session:
 
 
 def engine_register(params: Params, src, tgt, device: int = -1, history_cap: int = 1024, stop_flag=None,
-                    on_log=None, on_progress=None, stop_at: int = -1):
+                    on_log=None, on_progress=None, stop_at: int = -1, devices=None):
     """ICPEngine::registerPointClouds drop-in. Returns (rc, result, history, src_out).
     stop_at >= 0 raises the stop flag from the progress hook of that iteration (the reference's
     cross-thread ICPEngine::stop(), checked at the next iteration, icpengine.cpp:160)."""
@@ -517,12 +548,15 @@ def engine_register(params: Params, src, tgt, device: int = -1, history_cap: int
             pcb = PROGRESS_CB(_progress)
             keep.append(pcb)
             hooks.on_progress = pcb
-    rc = lib().icp_engine_register(C.byref(params), _ptr(src), src.shape[0], _ptr(tgt), tgt.shape[0], device,
-                                   C.byref(res), hist, history_cap, C.byref(hooks) if hooks else None)
+    devs = [device] if devices is None else list(devices)
+    ids = (C.c_int32 * len(devs))(*devs)
+    rc = lib().icp_engine_register_devices(C.byref(params), _ptr(src), src.shape[0], _ptr(tgt), tgt.shape[0],
+                                           len(devs), ids, C.byref(res), hist, history_cap,
+                                           C.byref(hooks) if hooks else None)
     return rc, res, [hist[k] for k in range(res.n_history)], src
 
 
-def cli_icp(src, tgt, max_iterations=20, tolerance=1e-2, device: int = -1):
+def cli_icp(src, tgt, max_iterations=20, tolerance=1e-2, device: int = -1, devices=None):
     """ICP() of icp_registration.cpp drop-in. Returns (R, t, transforms, src_out)."""
     src = _aos(src).copy()
     tgt = _aos(tgt)
@@ -531,8 +565,10 @@ def cli_icp(src, tgt, max_iterations=20, tolerance=1e-2, device: int = -1):
     cap = max(1, max_iterations)
     tr = np.zeros((cap, 16))
     n = C.c_int32()
-    _check(lib().icp_cli_icp(_ptr(src), src.shape[0], _ptr(tgt), tgt.shape[0], max_iterations, tolerance, _ptr(R),
-                             _ptr(t), _ptr(tr), cap, C.byref(n), device))
+    devs = [device] if devices is None else list(devices)
+    ids = (C.c_int32 * len(devs))(*devs)
+    _check(lib().icp_cli_icp_devices(_ptr(src), src.shape[0], _ptr(tgt), tgt.shape[0], max_iterations, tolerance,
+                                     _ptr(R), _ptr(t), _ptr(tr), cap, C.byref(n), len(devs), ids))
     return R.reshape(3, 3), t, tr[: n.value].reshape(-1, 4, 4), src
 
 

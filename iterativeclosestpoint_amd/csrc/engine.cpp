@@ -326,6 +326,12 @@ int icp_engine_run(icp_hip_ctx* ctx, const icp_params* p, icp_result* res, icp_i
 int icp_engine_register(const icp_params* p, double* src, int64_t n_src, const double* tgt, int64_t n_tgt,
                         int device, icp_result* res, icp_iteration_record* hist, int32_t cap,
                         const icp_engine_hooks* hooks) {
+  return icp_engine_register_devices(p, src, n_src, tgt, n_tgt, 1, &device, res, hist, cap, hooks);
+}
+
+int icp_engine_register_devices(const icp_params* p, double* src, int64_t n_src, const double* tgt, int64_t n_tgt,
+                                int n_devices, const int* device_ids, icp_result* res, icp_iteration_record* hist,
+                                int32_t cap, const icp_engine_hooks* hooks) {
   if (!p || !res) return ICP_HIP_EINVAL;
   std::memset(res, 0, sizeof(*res));
   if (!src || !tgt) {  // icpengine.cpp:26-29
@@ -336,9 +342,15 @@ int icp_engine_register(const icp_params* p, double* src, int64_t n_src, const d
     set_msg(res, "point cloud is empty");
     return ICP_HIP_EINVAL;
   }
+  if (n_devices < 1 || !device_ids) {
+    set_msg(res, "empty device list");
+    return ICP_HIP_EINVAL;
+  }
   const bool cli = p->rules == ICP_RULES_CLI;
   icp_hip_ctx* ctx = nullptr;
-  int rc = icp_hip_create(&ctx, device);
+  // one device: a plain context; several: one context over all of them (source shards, RCCL)
+  int rc = n_devices == 1 ? icp_hip_create(&ctx, device_ids[0])
+                          : icp_hip_create_multi(&ctx, n_devices, device_ids, nullptr, ICP_XPORT_AUTO);
   if (rc == ICP_HIP_OK)
     rc = icp_hip_set_target(ctx, tgt, n_tgt, cli ? 10 : p->octree_max_points, cli ? 20 : p->octree_max_depth,
                             p->rules);
@@ -348,7 +360,8 @@ int icp_engine_register(const icp_params* p, double* src, int64_t n_src, const d
     icp_hip_destroy(ctx);
     return rc;
   }
-  log_msg(hooks, "source: %lld points, target: %lld points", (long long)n_src, (long long)n_tgt);
+  log_msg(hooks, "source: %lld points, target: %lld points, %d device(s)", (long long)n_src, (long long)n_tgt,
+          n_devices);
   rc = icp_engine_run(ctx, p, res, hist, cap, hooks);
   // write back (icpengine.cpp:371-375): only when the engine finished; the CLI always writes
   // back what it has (icp_registration.cpp:609-613) — a CLI "too few" break is a success there.
@@ -367,6 +380,13 @@ int icp_engine_register(const icp_params* p, double* src, int64_t n_src, const d
 int icp_cli_icp(double* src, int64_t n_src, const double* tgt, int64_t n_tgt, int max_iterations, double tolerance,
                 double final_R[9], double final_t[3], double* iteration_transforms, int32_t cap, int32_t* n_transforms,
                 int device) {
+  return icp_cli_icp_devices(src, n_src, tgt, n_tgt, max_iterations, tolerance, final_R, final_t, iteration_transforms,
+                             cap, n_transforms, 1, &device);
+}
+
+int icp_cli_icp_devices(double* src, int64_t n_src, const double* tgt, int64_t n_tgt, int max_iterations,
+                        double tolerance, double final_R[9], double final_t[3], double* iteration_transforms,
+                        int32_t cap, int32_t* n_transforms, int n_devices, const int* device_ids) {
   icp_params p;
   icp_params_default(&p);
   p.max_iterations = max_iterations;
@@ -374,7 +394,8 @@ int icp_cli_icp(double* src, int64_t n_src, const double* tgt, int64_t n_tgt, in
   p.rules = ICP_RULES_CLI;
   std::vector<icp_iteration_record> hist((size_t)(max_iterations > 0 ? max_iterations : 1));
   icp_result res;
-  int rc = icp_engine_register(&p, src, n_src, tgt, n_tgt, device, &res, hist.data(), (int32_t)hist.size(), nullptr);
+  int rc = icp_engine_register_devices(&p, src, n_src, tgt, n_tgt, n_devices, device_ids, &res, hist.data(),
+                                       (int32_t)hist.size(), nullptr);
   if (rc != ICP_HIP_OK) return rc;
   for (int k = 0; k < 9; k++) final_R[k] = res.final_R[k];
   for (int k = 0; k < 3; k++) final_t[k] = res.final_t[k];

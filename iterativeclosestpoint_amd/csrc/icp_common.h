@@ -38,7 +38,8 @@ constexpr uint32_t kLeafBit = 0x80000000u;
 struct alignas(32) TgtPt {
   double x, y, z;
   int32_t orig;  // original index into the caller's target array
-  int32_t pad;
+  float sep;     // lower bound of the exact distance from this point to every other target point
+                 // (0 = none known; computed on the device after either build, k_target_sep)
 };
 static_assert(sizeof(TgtPt) == 32, "TgtPt must be 32 bytes");
 

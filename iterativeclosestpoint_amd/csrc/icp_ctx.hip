@@ -115,6 +115,7 @@ static NNLaunch base_launch(const icp_hip_ctx* c) {
   a.join_factor = c->cfg.join_factor;
   a.xcd_blocks = c->cfg.xcd_blocks;
   a.scan_groups = c->cfg.scan_groups;
+  a.certify_prev = c->cfg.certify_prev;
   a.dbg = c->dbg;
   for (int k = 0; k < 3; k++) {
     a.root_lo[k] = c->root_box[k];
@@ -163,6 +164,7 @@ int icp_hip_create_ex(icp_hip_ctx** out, int device, const icp_hip_config* cfg) 
   if (conf.candidate_cache != 0 && conf.candidate_cache != 1) return fail(ICP_HIP_EINVAL, "config: candidate_cache must be 0 or 1");
   if (conf.candidate_margin < 0 || conf.candidate_margin > 1024)
     return fail(ICP_HIP_EINVAL, "config: candidate_margin out of [0, 1024]");
+  if (conf.certify_prev < 0 || conf.certify_prev > 3) return fail(ICP_HIP_EINVAL, "config: certify_prev out of [0, 3]");
   if (!(conf.join_factor >= 1.0 && conf.join_factor <= 1e6))
     return fail(ICP_HIP_EINVAL, "config: join_factor out of [1, 1e6]");
   int ndev = 0;
@@ -204,6 +206,11 @@ int icp_hip_create_ex(icp_hip_ctx** out, int device, const icp_hip_config* cfg) 
 
 void icp_hip_destroy(icp_hip_ctx* c) {
   if (!c) return;
+  if (c->group) {
+    group_destroy(c);
+    delete c;
+    return;
+  }
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
   free_source(c);
@@ -234,6 +241,7 @@ int icp_hip_get_unique_id(uint8_t out[ICP_HIP_UNIQUE_ID_BYTES]) {
 }
 
 int icp_hip_comm_init(icp_hip_ctx* c, int nranks, int rank, const uint8_t id_bytes[ICP_HIP_UNIQUE_ID_BYTES]) {
+  if (c && c->group) return fail(ICP_HIP_EINVAL, "a multi-device context owns its communicators");
   if (!c || !id_bytes || nranks < 1 || rank < 0 || rank >= nranks) return fail(ICP_HIP_EINVAL, "bad comm arguments");
   HIP_TRY(hipSetDevice(c->device));
   // back to a world of one first: a failure below leaves no stale transport behind
@@ -257,7 +265,30 @@ int icp_hip_comm_init(icp_hip_ctx* c, int nranks, int rank, const uint8_t id_byt
   return ICP_HIP_OK;
 }
 
+}  // extern "C"
+
+int icp_ctx_attach_comm(icp_hip_ctx* c, ncclComm_t comm, int nranks, int rank) {
+  HIP_TRY(hipSetDevice(c->device));
+  if (c->comm) (void)ncclCommDestroy(c->comm);
+  c->comm = nullptr;
+  c->xfn = nullptr;
+  c->xuser = nullptr;
+  c->nranks = 1;
+  c->rank = 0;
+  dfree(c->gm);
+  dfree(c->gc);
+  HIP_TRY(dalloc(&c->gm, (size_t)nranks));
+  HIP_TRY(dalloc(&c->gc, (size_t)nranks));
+  c->comm = comm;
+  c->nranks = nranks;
+  c->rank = rank;
+  return ICP_HIP_OK;
+}
+
+extern "C" {
+
 int icp_hip_comm_init_host(icp_hip_ctx* c, int nranks, int rank, icp_hip_exchange_fn exchange, void* user) {
+  if (c && c->group) return fail(ICP_HIP_EINVAL, "a multi-device context owns its communicators");
   if (!c || nranks < 1 || rank < 0 || rank >= nranks || (nranks > 1 && !exchange))
     return fail(ICP_HIP_EINVAL, "bad comm arguments");
   HIP_TRY(hipSetDevice(c->device));
@@ -298,6 +329,8 @@ static int all_gather_record(icp_hip_ctx* c, const double* d_local, double* d_ga
 
 int icp_hip_set_target(icp_hip_ctx* c, const double* xyz, int64_t n, int max_points, int max_depth, int rules) {
   if (!c || (!xyz && n > 0)) return fail(ICP_HIP_EINVAL, "null argument");
+  if (c->group) return n <= 0 ? fail(ICP_HIP_EINVAL, "empty target cloud (icpengine.cpp:31-34 rejects it)")
+                             : group_set_target(c, xyz, n, max_points, max_depth, rules);
   if (n <= 0) return fail(ICP_HIP_EINVAL, "empty target cloud (icpengine.cpp:31-34 rejects it)");
   if (max_depth < 0 || max_depth > 60) return fail(ICP_HIP_EINVAL, "max_depth out of range [0, 60]");
   if (n > (int64_t)0x7fffffff) return fail(ICP_HIP_EINVAL, "target size out of range (int32 indices, as the reference)");
@@ -342,6 +375,8 @@ int icp_hip_set_target(icp_hip_ctx* c, const double* xyz, int64_t n, int max_poi
     c->max_depth = t.max_depth;
     c->levels = t.max_inner_depth + 1 > 0 ? t.max_inner_depth + 1 : 1;
   }
+  // separation of every target point (the previous-match certificate, certify_prev)
+  if (c->cfg.certify_prev) HIP_TRY(launch_target_sep(c->nodes, c->pts, n, c->levels, c->stream));
   // root box (host copy: the kernels' cell arithmetic starts from it) and the cell tables
   {
     NodeRec root;
@@ -374,6 +409,7 @@ int icp_hip_set_target(icp_hip_ctx* c, const double* xyz, int64_t n, int max_poi
 
 int icp_hip_target_build_info(icp_hip_ctx* c, int32_t* on_device, double* build_ms) {
   if (!c) return fail(ICP_HIP_EINVAL, "null context");
+  if (c->group) return group_target_build_info(c, on_device, build_ms);
   if (!c->nodes) return fail(ICP_HIP_ENOTREADY, "target not set");
   if (on_device) *on_device = c->target_on_device;
   if (build_ms) *build_ms = c->target_build_ms;
@@ -383,6 +419,7 @@ int icp_hip_target_build_info(icp_hip_ctx* c, int32_t* on_device, double* build_
 int icp_hip_copy_target(icp_hip_ctx* c, double* box6, int32_t* first, uint32_t* meta, int32_t* depth, double* xyz,
                         int32_t* orig) {
   if (!c) return fail(ICP_HIP_EINVAL, "null context");
+  if (c->group) return icp_hip_copy_target(group_member(c, 0), box6, first, meta, depth, xyz, orig);
   if (!c->nodes) return fail(ICP_HIP_ENOTREADY, "target not set");
   HIP_TRY(hipSetDevice(c->device));
   std::vector<NodeRec> nodes((size_t)c->n_nodes);
@@ -412,8 +449,21 @@ int icp_hip_copy_target(icp_hip_ctx* c, double* box6, int32_t* first, uint32_t* 
   return ICP_HIP_OK;
 }
 
+int icp_hip_target_separation(icp_hip_ctx* c, float* sep_out) {
+  if (!c || !sep_out) return fail(ICP_HIP_EINVAL, "null argument");
+  if (c->group) return icp_hip_target_separation(group_member(c, 0), sep_out);
+  if (!c->nodes) return fail(ICP_HIP_ENOTREADY, "target not set");
+  HIP_TRY(hipSetDevice(c->device));
+  std::vector<TgtPt> pts((size_t)c->n_tgt);
+  HIP_TRY(hipMemcpyAsync(pts.data(), c->pts, pts.size() * sizeof(TgtPt), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  for (const TgtPt& p : pts) sep_out[p.orig] = p.sep;
+  return ICP_HIP_OK;
+}
+
 int icp_hip_set_source(icp_hip_ctx* c, const double* xyz, int64_t n) {
   if (!c || (!xyz && n > 0) || n < 0) return fail(ICP_HIP_EINVAL, "bad source arguments");
+  if (c->group) return group_set_source(c, xyz, n);
   if (n > (int64_t)0x7fffffff) return fail(ICP_HIP_EINVAL, "source shard larger than INT32_MAX points");
   HIP_TRY(hipSetDevice(c->device));
   free_source(c);
@@ -464,6 +514,7 @@ int icp_hip_set_source(icp_hip_ctx* c, const double* xyz, int64_t n) {
 int icp_hip_iterate(icp_hip_ctx* c, const double* T_apply, int iter, int rules, double sigma_multiplier,
                     icp_iter_stats* out) {
   if (!c || !out) return fail(ICP_HIP_EINVAL, "null argument");
+  if (c->group) return group_iterate(c, T_apply, iter, rules, sigma_multiplier, out);
   if (!c->nodes) return fail(ICP_HIP_ENOTREADY, "target not set");
   if (!c->x && c->n_src > 0) return fail(ICP_HIP_ENOTREADY, "source not set");
   HIP_TRY(hipSetDevice(c->device));
@@ -541,6 +592,7 @@ int icp_hip_iterate(icp_hip_ctx* c, const double* T_apply, int iter, int rules, 
     auto published = [&]() { return __atomic_load_n(word, __ATOMIC_ACQUIRE) == want_bits; };
     for (unsigned spin = 1; !published(); spin++) {
       if ((spin & 1023u) == 0) {
+        if (c->abort && c->abort->load()) return fail(ICP_HIP_EEXCHANGE, "iterate: a peer device of the group failed");
         const hipError_t q = hipStreamQuery(s);
         if (q == hipSuccess && published()) break;
         if (q == hipSuccess) return fail(ICP_HIP_EDEVICE, "iterate: stream idle but the record was not published");
@@ -577,6 +629,7 @@ int icp_hip_iterate(icp_hip_ctx* c, const double* T_apply, int iter, int rules, 
 
 int icp_hip_debug_counters(icp_hip_ctx* c, uint64_t out[ICP_DBG_SLOTS]) {
   if (!c || !out) return fail(ICP_HIP_EINVAL, "null argument");
+  if (c->group) return group_debug_counters(c, out);
   std::memset(out, 0, ICP_DBG_SLOTS * sizeof(uint64_t));
   if (!c->dbg) return ICP_HIP_OK;
   HIP_TRY(hipSetDevice(c->device));
@@ -587,6 +640,7 @@ int icp_hip_debug_counters(icp_hip_ctx* c, uint64_t out[ICP_DBG_SLOTS]) {
 
 int icp_hip_apply(icp_hip_ctx* c, const double* T) {
   if (!c || !T) return fail(ICP_HIP_EINVAL, "null argument");
+  if (c->group) return group_apply(c, T);
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(launch_apply(T, c->x, c->y, c->z, c->n_src, c->stream));
   c->have_prev = false;  // queries moved without a search: previous residuals are no guess
@@ -595,6 +649,7 @@ int icp_hip_apply(icp_hip_ctx* c, const double* T) {
 }
 
 int icp_hip_get_source(icp_hip_ctx* c, double* xyz_out) {
+  if (c && c->group) return xyz_out ? group_get_source(c, xyz_out) : fail(ICP_HIP_EINVAL, "null argument");
   if (!c || (!xyz_out && c->n_src > 0)) return fail(ICP_HIP_EINVAL, "null argument");
   if (c->n_src == 0) return ICP_HIP_OK;
   HIP_TRY(hipSetDevice(c->device));
@@ -610,6 +665,7 @@ int icp_hip_get_source(icp_hip_ctx* c, double* xyz_out) {
 
 int icp_hip_get_correspondences(icp_hip_ctx* c, int32_t* idx_out, double* dist_out) {
   if (!c) return fail(ICP_HIP_EINVAL, "null argument");
+  if (c->group) return group_get_correspondences(c, idx_out, dist_out);
   if (!c->have_results) return fail(ICP_HIP_ENOTREADY, "no iteration has run on this source");
   if (c->n_src == 0) return ICP_HIP_OK;
   HIP_TRY(hipSetDevice(c->device));
@@ -630,6 +686,7 @@ int icp_hip_get_correspondences(icp_hip_ctx* c, int32_t* idx_out, double* dist_o
 
 int icp_hip_nn(icp_hip_ctx* c, const double* q, int64_t n, int32_t* idx_out, double* dist_out) {
   if (!c || n < 0 || (n > 0 && !q)) return fail(ICP_HIP_EINVAL, "bad arguments");
+  if (c->group) return icp_hip_nn(group_member(c, 0), q, n, idx_out, dist_out);  // the replicated octree
   if (!c->nodes) return fail(ICP_HIP_ENOTREADY, "target not set");
   if (n == 0) return ICP_HIP_OK;
   if (n > (int64_t)0x7fffffff) return fail(ICP_HIP_EINVAL, "too many queries");
@@ -681,6 +738,7 @@ int icp_hip_nn(icp_hip_ctx* c, const double* q, int64_t n, int32_t* idx_out, dou
 
 int icp_hip_traversal_counts(icp_hip_ctx* c, double* mean_entries, double* mean_points) {
   if (!c || !mean_entries || !mean_points) return fail(ICP_HIP_EINVAL, "null argument");
+  if (c->group) return group_traversal_counts(c, mean_entries, mean_points);
   if (!c->nodes || (!c->x && c->n_src > 0)) return fail(ICP_HIP_ENOTREADY, "target/source not set");
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipMemsetAsync(c->counters, 0, 2 * sizeof(unsigned long long), c->stream));
@@ -705,6 +763,7 @@ int icp_hip_traversal_counts(icp_hip_ctx* c, double* mean_entries, double* mean_
 
 int icp_hip_target_info(icp_hip_ctx* c, int64_t* n_nodes, int64_t* n_leaves, int32_t* max_depth, int32_t* levels) {
   if (!c) return fail(ICP_HIP_EINVAL, "null ctx");
+  if (c->group) return icp_hip_target_info(group_member(c, 0), n_nodes, n_leaves, max_depth, levels);
   if (n_nodes) *n_nodes = c->n_nodes;
   if (n_leaves) *n_leaves = c->n_leaves;
   if (max_depth) *max_depth = c->max_depth;
@@ -714,6 +773,7 @@ int icp_hip_target_info(icp_hip_ctx* c, int64_t* n_nodes, int64_t* n_leaves, int
 
 int icp_hip_timings(icp_hip_ctx* c, int k, double* nn_ms, double* it_ms) {
   if (!c || k < 0) return fail(ICP_HIP_EINVAL, "bad arguments");
+  if (c->group) return group_timings(c, k, nn_ms, it_ms);
   if (k > icp_hip_ctx::kTimingRing || k > c->n_iterates) return fail(ICP_HIP_EINVAL, "fewer iterates recorded than asked");
   HIP_TRY(hipSetDevice(c->device));
   for (int j = 0; j < k; j++) {
@@ -730,12 +790,14 @@ int icp_hip_timings(icp_hip_ctx* c, int k, double* nn_ms, double* it_ms) {
 
 int icp_hip_last_timing(icp_hip_ctx* c, double* nn_ms, double* it_ms) {
   if (!c) return fail(ICP_HIP_EINVAL, "null ctx");
+  if (c->group) return group_timings(c, 1, nn_ms, it_ms);
   if (c->n_iterates == 0) return fail(ICP_HIP_ENOTREADY, "no iterate has run");
   return icp_hip_timings(c, 1, nn_ms, it_ms);
 }
 
 int icp_hip_synchronize(icp_hip_ctx* c) {
   if (!c) return fail(ICP_HIP_EINVAL, "null ctx");
+  if (c->group) return group_synchronize(c);
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipStreamSynchronize(c->stream));
   return ICP_HIP_OK;

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <atomic>
 #include <cstdint>
 
 #include "../../include/icp_hip.h"
@@ -68,6 +69,31 @@ struct icp_hip_ctx {
   void* xuser = nullptr;
   icp::Moments* gm = nullptr;
   icp::CovMoments* gc = nullptr;
+  // a member of a multi-device context: set when a peer member failed (the waits give up)
+  const std::atomic<int>* abort = nullptr;
+
+  // multi-device context (icp_hip_create_multi): the member contexts and their driver threads
+  // (icp_group.cpp); the single-device fields above are then unused
+  struct DeviceGroup* group = nullptr;
 };
 
 void icp_ctx_set_error(const char* msg);
+// Attach a communicator created elsewhere (ncclCommInitAll of a multi-device context); the
+// context owns it from then on.
+int icp_ctx_attach_comm(icp_hip_ctx* c, ncclComm_t comm, int nranks, int rank);
+
+// The multi-device context (icp_group.cpp): every C-ABI entry point of icp_ctx.hip dispatches here
+// when ctx->group is set.
+void group_destroy(icp_hip_ctx* c);
+int group_set_target(icp_hip_ctx* c, const double* xyz, int64_t n, int max_points, int max_depth, int rules);
+int group_target_build_info(icp_hip_ctx* c, int32_t* on_device, double* build_ms);
+int group_set_source(icp_hip_ctx* c, const double* xyz, int64_t n);
+int group_iterate(icp_hip_ctx* c, const double* T_apply, int iter, int rules, double sigma, icp_iter_stats* out);
+int group_apply(icp_hip_ctx* c, const double* T);
+int group_get_source(icp_hip_ctx* c, double* xyz_out);
+int group_get_correspondences(icp_hip_ctx* c, int32_t* idx_out, double* dist_out);
+int group_traversal_counts(icp_hip_ctx* c, double* mean_entries, double* mean_points);
+int group_timings(icp_hip_ctx* c, int k, double* nn_ms, double* it_ms);
+int group_debug_counters(icp_hip_ctx* c, uint64_t out[ICP_DBG_SLOTS]);
+int group_synchronize(icp_hip_ctx* c);
+icp_hip_ctx* group_member(icp_hip_ctx* c, int k);

@@ -1,0 +1,418 @@
+// icp_group.cpp — a context that drives several GPUs from one process (icp_hip_create_multi).
+//
+// the drop-in's callers (ICPEngine::registerPointClouds, icpengine.cpp:24-60;
+// the CLI's ICP(), icp_registration.cpp:443-446) are single-process, so the multi-GPU path must be
+// reachable from one process. A group holds one member context per device (icp_ctx.hip: a
+// replicated octree, a spatially compact shard of the source) and one driver thread per member.
+// An iterate runs every member's ordinary multi-rank iterate concurrently, each on its own thread:
+// the two per-iteration all-gathers are RCCL collectives over communicators from ncclCommInitAll
+// (one per device), or, when devices repeat (RCCL refuses two ranks on one device) or the caller
+// asks for it, an in-process host gather with the same record layout. Every member merges the
+// gathered records in rank order on its device, so all members hold bitwise-identical statistics
+// (the same numbers a world of N processes computes).
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <condition_variable>
+#include <cstring>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/icp_hip.h"
+#include "icp_ctx_internal.h"
+#include "query_order.h"
+
+namespace {
+
+// A persistent driver thread: runs one posted job at a time.
+class Driver {
+ public:
+  Driver() : th_([this] { loop(); }) {}
+  ~Driver() {
+    {
+      std::lock_guard<std::mutex> g(m_);
+      quit_ = true;
+    }
+    cv_.notify_all();
+    th_.join();
+  }
+  void post(std::function<void()> f) {
+    {
+      std::lock_guard<std::mutex> g(m_);
+      job_ = std::move(f);
+      busy_ = true;
+    }
+    cv_.notify_all();
+  }
+  void wait() {
+    std::unique_lock<std::mutex> g(m_);
+    cv_.wait(g, [this] { return !busy_; });
+  }
+
+ private:
+  void loop() {
+    std::unique_lock<std::mutex> g(m_);
+    while (true) {
+      cv_.wait(g, [this] { return quit_ || (busy_ && job_); });
+      if (quit_) return;
+      auto f = std::move(job_);
+      job_ = nullptr;
+      g.unlock();
+      f();
+      g.lock();
+      busy_ = false;
+      cv_.notify_all();
+    }
+  }
+  std::mutex m_;
+  std::condition_variable cv_;
+  std::function<void()> job_;
+  bool busy_ = false, quit_ = false;
+  std::thread th_;  // last: started once the members above exist
+};
+
+// In-process all-gather of one record per member (the host transport): members deposit their
+// record, the last arrival publishes the generation, everyone copies the gathered array. Two
+// buffers alternate by generation: exchange k+2 can only start after every member has finished
+// copying exchange k (it had to arrive at k+1 first).
+struct LocalExchange {
+  int n = 0;
+  std::mutex m;
+  std::condition_variable cv;
+  int arrived = 0;
+  uint64_t gen = 0;
+  std::vector<double> buf[2];
+  const std::atomic<int>* abort = nullptr;
+
+  int gather(int rank, const double* local, int count, double* gathered) {
+    std::unique_lock<std::mutex> g(m);
+    std::vector<double>& b = buf[gen & 1];
+    if (b.size() < (size_t)n * count) b.resize((size_t)n * count);
+    std::memcpy(b.data() + (size_t)rank * count, local, sizeof(double) * count);
+    const uint64_t my = gen;
+    if (++arrived == n) {
+      arrived = 0;
+      gen++;
+      cv.notify_all();
+    } else {
+      cv.wait(g, [&] { return gen != my || (abort && abort->load()); });
+      if (gen == my) return 1;  // a peer member failed
+    }
+    std::memcpy(gathered, b.data(), sizeof(double) * (size_t)n * count);
+    return 0;
+  }
+  void wake() {
+    std::lock_guard<std::mutex> g(m);
+    cv.notify_all();
+  }
+};
+
+struct ExchangeSlot {
+  LocalExchange* x;
+  int rank;
+};
+
+int local_exchange(void* user, const double* local, int32_t count, double* gathered) {
+  auto* s = static_cast<ExchangeSlot*>(user);
+  return s->x->gather(s->rank, local, count, gathered);
+}
+
+}  // namespace
+
+struct DeviceGroup {
+  std::vector<icp_hip_ctx*> members;
+  std::vector<int> devices;
+  int transport = ICP_XPORT_HOST;
+  std::unique_ptr<LocalExchange> lx;
+  std::vector<ExchangeSlot> slots;
+  std::vector<std::unique_ptr<Driver>> drivers;
+  std::atomic<int> abort{0};
+  // the source: caller index of group slot k, and member m's slots [lo[m], lo[m + 1])
+  std::vector<int32_t> order;
+  std::vector<int64_t> lo;
+  int64_t n_src = 0;
+};
+
+namespace {
+
+int fail(int code, const std::string& msg) {
+  icp_ctx_set_error(msg.c_str());
+  return code;
+}
+
+// f(k, member) on every member's driver thread, concurrently; the first failure's code and message
+// (the message is thread-local to the driver that saw it) come back to the caller. A failing member
+// raises the group's abort flag, so peers waiting in an exchange or for a record give up.
+int for_members(DeviceGroup* g, const std::function<int(int, icp_hip_ctx*)>& f) {
+  const int n = (int)g->members.size();
+  std::vector<int> rc((size_t)n, ICP_HIP_OK);
+  std::vector<std::string> msg((size_t)n);
+  for (int k = 0; k < n; k++) {
+    g->drivers[k]->post([g, k, &f, &rc, &msg] {
+      rc[k] = f(k, g->members[k]);
+      if (rc[k] != ICP_HIP_OK) {
+        msg[k] = icp_hip_last_error();
+        g->abort.store(1);
+        if (g->lx) g->lx->wake();
+      }
+    });
+  }
+  for (int k = 0; k < n; k++) g->drivers[k]->wait();
+  // report the root cause: a member's own failure before a peer's "peer failed"
+  int first = -1;
+  for (int k = 0; k < n; k++)
+    if (rc[k] != ICP_HIP_OK && (first < 0 || (rc[first] == ICP_HIP_EEXCHANGE && rc[k] != ICP_HIP_EEXCHANGE))) first = k;
+  if (first < 0) return ICP_HIP_OK;
+  return fail(rc[first], "device " + std::to_string(g->devices[first]) + ": " + msg[first]);
+}
+
+void shard_ranges(int64_t n, int w, std::vector<int64_t>* lo) {
+  lo->assign((size_t)w + 1, 0);
+  const int64_t base = n / w, rem = n % w;
+  for (int r = 0; r < w; r++) (*lo)[r + 1] = (*lo)[r] + base + (r < rem ? 1 : 0);
+}
+
+}  // namespace
+
+extern "C" int icp_hip_create_multi(icp_hip_ctx** out, int n_devices, const int* device_ids,
+                                    const icp_hip_config* cfg, int transport) {
+  if (!out) return fail(ICP_HIP_EINVAL, "null out");
+  *out = nullptr;
+  if (n_devices < 1 || n_devices > 64 || !device_ids) return fail(ICP_HIP_EINVAL, "create_multi: bad device list");
+  if (transport != ICP_XPORT_AUTO && transport != ICP_XPORT_RCCL && transport != ICP_XPORT_HOST)
+    return fail(ICP_HIP_EINVAL, "create_multi: unknown transport");
+  std::vector<int> devs(device_ids, device_ids + n_devices);
+  std::vector<int> sorted = devs;
+  std::sort(sorted.begin(), sorted.end());
+  const bool distinct = std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end();
+  if (transport == ICP_XPORT_RCCL && !distinct)
+    return fail(ICP_HIP_EINVAL, "create_multi: RCCL needs distinct devices (one rank per GPU)");
+  if (transport == ICP_XPORT_AUTO) {
+    if (n_devices == 1) return icp_hip_create_ex(out, devs[0], cfg);  // a plain single-device context
+    transport = distinct ? ICP_XPORT_RCCL : ICP_XPORT_HOST;
+  }
+  auto* g = new DeviceGroup();
+  g->devices = devs;
+  g->transport = transport;
+  auto* c = new icp_hip_ctx();
+  c->device = devs[0];
+  c->group = g;
+  if (cfg) c->cfg = *cfg;
+  else icp_hip_config_default(&c->cfg);
+  int rc = ICP_HIP_OK;
+  for (int k = 0; k < n_devices && rc == ICP_HIP_OK; k++) {
+    icp_hip_ctx* m = nullptr;
+    rc = icp_hip_create_ex(&m, devs[k], cfg);
+    if (rc == ICP_HIP_OK) {
+      m->abort = &g->abort;
+      g->members.push_back(m);
+    }
+  }
+  if (rc == ICP_HIP_OK && transport == ICP_XPORT_RCCL) {
+    std::vector<ncclComm_t> comms((size_t)n_devices, nullptr);
+    const ncclResult_t r = ncclCommInitAll(comms.data(), n_devices, devs.data());
+    if (r != ncclSuccess) {
+      rc = fail(ICP_HIP_ERCCL, std::string("ncclCommInitAll: ") + ncclGetErrorString(r));
+    } else {
+      for (int k = 0; k < n_devices; k++) {
+        const int rk = icp_ctx_attach_comm(g->members[k], comms[k], n_devices, k);
+        if (rk != ICP_HIP_OK && rc == ICP_HIP_OK) rc = rk;
+        if (rk != ICP_HIP_OK) (void)ncclCommDestroy(comms[k]);
+      }
+    }
+  } else if (rc == ICP_HIP_OK) {
+    g->lx = std::make_unique<LocalExchange>();
+    g->lx->n = n_devices;
+    g->lx->abort = &g->abort;
+    g->slots.resize((size_t)n_devices);
+    for (int k = 0; k < n_devices && rc == ICP_HIP_OK; k++) {
+      g->slots[k] = ExchangeSlot{g->lx.get(), k};
+      rc = icp_hip_comm_init_host(g->members[k], n_devices, k, &local_exchange, &g->slots[k]);
+    }
+  }
+  if (rc == ICP_HIP_OK)
+    for (int k = 0; k < n_devices; k++) g->drivers.push_back(std::make_unique<Driver>());
+  if (rc != ICP_HIP_OK) {
+    const std::string why = icp_hip_last_error();
+    icp_hip_destroy(c);
+    return fail(rc, why);
+  }
+  *out = c;
+  return ICP_HIP_OK;
+}
+
+void group_destroy(icp_hip_ctx* c) {
+  DeviceGroup* g = c->group;
+  g->drivers.clear();  // joins the driver threads
+  for (icp_hip_ctx* m : g->members) icp_hip_destroy(m);
+  delete g;
+  c->group = nullptr;
+}
+
+icp_hip_ctx* group_member(icp_hip_ctx* c, int k) { return c->group->members[k]; }
+
+int group_set_target(icp_hip_ctx* c, const double* xyz, int64_t n, int max_points, int max_depth, int rules) {
+  // every device builds the same octree from the same cloud (a replica each)
+  return for_members(c->group, [&](int, icp_hip_ctx* m) {
+    return icp_hip_set_target(m, xyz, n, max_points, max_depth, rules);
+  });
+}
+
+int group_target_build_info(icp_hip_ctx* c, int32_t* on_device, double* build_ms) {
+  double worst = 0.0;
+  int32_t od = 1;
+  for (icp_hip_ctx* m : c->group->members) {
+    int32_t o = 0;
+    double ms = 0.0;
+    const int rc = icp_hip_target_build_info(m, &o, &ms);
+    if (rc != ICP_HIP_OK) return rc;
+    od = od && o;
+    worst = ms > worst ? ms : worst;
+  }
+  if (on_device) *on_device = od;
+  if (build_ms) *build_ms = worst;
+  return ICP_HIP_OK;
+}
+
+int group_set_source(icp_hip_ctx* c, const double* xyz, int64_t n) {
+  DeviceGroup* g = c->group;
+  const int w = (int)g->members.size();
+  if (n < w) return fail(ICP_HIP_EINVAL, "set_source: a multi-device context needs at least one point per device");
+  // spatially compact shards: contiguous ranges of the kd order (icp_source_shard_order)
+  icp::kd_query_order(xyz, n, 8, &g->order);
+  shard_ranges(n, w, &g->lo);
+  g->n_src = n;
+  return for_members(g, [&](int k, icp_hip_ctx* m) {
+    const int64_t a = g->lo[k], b = g->lo[k + 1];
+    std::vector<double> shard((size_t)(3 * (b - a)));
+    for (int64_t j = a; j < b; j++) std::memcpy(&shard[3 * (j - a)], xyz + 3 * (int64_t)g->order[j], 3 * sizeof(double));
+    return icp_hip_set_source(m, shard.data(), b - a);
+  });
+}
+
+int group_iterate(icp_hip_ctx* c, const double* T_apply, int iter, int rules, double sigma, icp_iter_stats* out) {
+  DeviceGroup* g = c->group;
+  const int w = (int)g->members.size();
+  std::vector<icp_iter_stats> st((size_t)w);
+  const int rc = for_members(g, [&](int k, icp_hip_ctx* m) { return icp_hip_iterate(m, T_apply, iter, rules, sigma, &st[k]); });
+  if (rc != ICP_HIP_OK) return rc;
+  // the statistics are merged in rank order on every device: identical on all members
+  for (int k = 1; k < w; k++)
+    if (st[k].valid != st[0].valid || std::memcmp(&st[k].mean, &st[0].mean, sizeof(double)) != 0 ||
+        std::memcmp(st[k].H, st[0].H, sizeof(st[0].H)) != 0)
+      return fail(ICP_HIP_EDEVICE, "iterate: members disagree on the merged statistics");
+  *out = st[0];
+  out->n_fallback = out->n_lane_search = out->n_ball_search = 0;  // per-rank counts: summed
+  for (const icp_iter_stats& s : st) {
+    out->n_fallback += s.n_fallback;
+    out->n_lane_search += s.n_lane_search;
+    out->n_ball_search += s.n_ball_search;
+  }
+  return ICP_HIP_OK;
+}
+
+int group_apply(icp_hip_ctx* c, const double* T) {
+  return for_members(c->group, [&](int, icp_hip_ctx* m) { return icp_hip_apply(m, T); });
+}
+
+int group_get_source(icp_hip_ctx* c, double* xyz_out) {
+  DeviceGroup* g = c->group;
+  return for_members(g, [&](int k, icp_hip_ctx* m) {
+    const int64_t a = g->lo[k], b = g->lo[k + 1];
+    std::vector<double> shard((size_t)(3 * (b - a)));
+    const int rc = icp_hip_get_source(m, shard.data());
+    if (rc != ICP_HIP_OK) return rc;
+    for (int64_t j = a; j < b; j++) std::memcpy(xyz_out + 3 * (int64_t)g->order[j], &shard[3 * (j - a)], 3 * sizeof(double));
+    return ICP_HIP_OK;
+  });
+}
+
+int group_get_correspondences(icp_hip_ctx* c, int32_t* idx_out, double* dist_out) {
+  DeviceGroup* g = c->group;
+  return for_members(g, [&](int k, icp_hip_ctx* m) {
+    const int64_t a = g->lo[k], b = g->lo[k + 1];
+    std::vector<int32_t> idx(idx_out ? (size_t)(b - a) : 0);
+    std::vector<double> d(dist_out ? (size_t)(b - a) : 0);
+    const int rc = icp_hip_get_correspondences(m, idx_out ? idx.data() : nullptr, dist_out ? d.data() : nullptr);
+    if (rc != ICP_HIP_OK) return rc;
+    for (int64_t j = a; j < b; j++) {
+      if (idx_out) idx_out[g->order[j]] = idx[j - a];
+      if (dist_out) dist_out[g->order[j]] = d[j - a];
+    }
+    return ICP_HIP_OK;
+  });
+}
+
+int group_traversal_counts(icp_hip_ctx* c, double* mean_entries, double* mean_points) {
+  DeviceGroup* g = c->group;
+  const int w = (int)g->members.size();
+  std::vector<double> e((size_t)w), p((size_t)w);
+  const int rc = for_members(g, [&](int k, icp_hip_ctx* m) { return icp_hip_traversal_counts(m, &e[k], &p[k]); });
+  if (rc != ICP_HIP_OK) return rc;
+  double se = 0.0, sp = 0.0;
+  for (int k = 0; k < w; k++) {
+    const double nk = (double)(g->lo[k + 1] - g->lo[k]);
+    se += e[k] * nk;
+    sp += p[k] * nk;
+  }
+  const double n = g->n_src > 0 ? (double)g->n_src : 1.0;
+  *mean_entries = se / n;
+  *mean_points = sp / n;
+  return ICP_HIP_OK;
+}
+
+int group_timings(icp_hip_ctx* c, int k, double* nn_ms, double* it_ms) {
+  // per iterate, the slowest member (the iterate ends when every member's record is published)
+  std::vector<double> a((size_t)k), b((size_t)k);
+  bool first = true;
+  for (icp_hip_ctx* m : c->group->members) {
+    const int rc = icp_hip_timings(m, k, a.data(), b.data());
+    if (rc != ICP_HIP_OK) return rc;
+    for (int j = 0; j < k; j++) {
+      if (nn_ms) nn_ms[j] = first || a[j] > nn_ms[j] ? a[j] : nn_ms[j];
+      if (it_ms) it_ms[j] = first || b[j] > it_ms[j] ? b[j] : it_ms[j];
+    }
+    first = false;
+  }
+  return ICP_HIP_OK;
+}
+
+int group_debug_counters(icp_hip_ctx* c, uint64_t out[ICP_DBG_SLOTS]) {
+  std::memset(out, 0, ICP_DBG_SLOTS * sizeof(uint64_t));
+  for (icp_hip_ctx* m : c->group->members) {
+    uint64_t v[ICP_DBG_SLOTS];
+    const int rc = icp_hip_debug_counters(m, v);
+    if (rc != ICP_HIP_OK) return rc;
+    for (int s = 0; s < ICP_DBG_SLOTS; s++) out[s] += v[s];
+  }
+  return ICP_HIP_OK;
+}
+
+int group_synchronize(icp_hip_ctx* c) {
+  for (icp_hip_ctx* m : c->group->members) {
+    const int rc = icp_hip_synchronize(m);
+    if (rc != ICP_HIP_OK) return rc;
+  }
+  return ICP_HIP_OK;
+}
+
+extern "C" int icp_hip_ctx_devices(icp_hip_ctx* c, int32_t* n_devices, int32_t* device_ids, int32_t cap,
+                                   int32_t* transport) {
+  if (!c) return fail(ICP_HIP_EINVAL, "null context");
+  if (c->group) {
+    const DeviceGroup* g = c->group;
+    if (n_devices) *n_devices = (int32_t)g->devices.size();
+    for (int k = 0; device_ids && k < (int)g->devices.size() && k < cap; k++) device_ids[k] = g->devices[k];
+    if (transport) *transport = g->transport;
+    return ICP_HIP_OK;
+  }
+  if (n_devices) *n_devices = 1;
+  if (device_ids && cap > 0) device_ids[0] = c->device;
+  if (transport) *transport = c->comm ? ICP_XPORT_RCCL : c->xfn ? ICP_XPORT_CALLBACK : ICP_XPORT_AUTO;
+  return ICP_HIP_OK;
+}

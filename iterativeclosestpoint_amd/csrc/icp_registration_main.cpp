@@ -5,7 +5,10 @@
 //
 //   icp_registration [--source Scan_096_origin.las] [--target Scannew_099.las]
 //                    [--sample-rate 50] [--max-iters 20] [--tolerance 1e-2]
-//                    [--outdir .] [--device 0] [--pause]
+//                    [--outdir .] [--device 0 | --devices 0,1,...] [--pause]
+//
+// --devices runs one registration over several GPUs of this process (icp_cli_icp_devices: the
+// source sharded over them, the octree replicated, RCCL all-gathers per iteration).
 //
 // Exit code 255 (the reference's `return -1`) when an input cannot be read.
 #include <cstdio>
@@ -28,14 +31,14 @@ struct Args {
   int max_iters = 20;                           // :900
   double tolerance = 1e-2;                      // :901
   std::string outdir = ".";
-  int device = 0;
+  std::vector<int> devices{0};
   bool pause = false;
 };
 
 [[noreturn]] void usage(const char* prog, int code) {
   std::fprintf(code ? stderr : stdout,
                "usage: %s [--source F] [--target F] [--sample-rate N] [--max-iters N] [--tolerance X]\n"
-               "          [--outdir D] [--device N] [--pause]\n",
+               "          [--outdir D] [--device N | --devices N,M,...] [--pause]\n",
                prog);
   std::exit(code);
 }
@@ -54,7 +57,22 @@ Args parse(int argc, char** argv) {
     else if (k == "--max-iters") a.max_iters = (int)std::strtol(val(), nullptr, 10);
     else if (k == "--tolerance") a.tolerance = std::strtod(val(), nullptr);
     else if (k == "--outdir") a.outdir = val();
-    else if (k == "--device") a.device = (int)std::strtol(val(), nullptr, 10);
+    else if (k == "--device") a.devices = {(int)std::strtol(val(), nullptr, 10)};
+    else if (k == "--devices") {
+      a.devices.clear();
+      std::string list = val();
+      size_t p = 0;
+      while (p <= list.size()) {
+        const size_t q = list.find(',', p);
+        const std::string tok = list.substr(p, q == std::string::npos ? std::string::npos : q - p);
+        char* end = nullptr;
+        const long d = std::strtol(tok.c_str(), &end, 10);
+        if (tok.empty() || *end != '\0' || d < 0) usage(argv[0], 2);
+        a.devices.push_back((int)d);
+        if (q == std::string::npos) break;
+        p = q + 1;
+      }
+    }
     else if (k == "--pause") a.pause = true;
     else if (k == "-h" || k == "--help") usage(argv[0], 0);
     else usage(argv[0], 2);
@@ -120,8 +138,9 @@ int main(int argc, char** argv) {
   const int cap = a.max_iters > 0 ? a.max_iters : 1;
   std::vector<double> transforms((size_t)cap * 16);
   int32_t n_tr = 0;
-  const int rc = icp_cli_icp(ss.data(), ns, ts.data(), nt, a.max_iters, a.tolerance, R, t, transforms.data(), cap,
-                             &n_tr, a.device);
+  if (a.devices.size() > 1) std::cout << "devices: " << a.devices.size() << " GPUs" << std::endl;
+  const int rc = icp_cli_icp_devices(ss.data(), ns, ts.data(), nt, a.max_iters, a.tolerance, R, t, transforms.data(),
+                                     cap, &n_tr, (int)a.devices.size(), a.devices.data());
   if (rc != 0) {
     std::cerr << "ICP failed (" << rc << "): " << icp_hip_last_error() << std::endl;
     return fail(a, "registration failed");

@@ -74,11 +74,14 @@ struct NNLaunch {
   uint32_t wc_gen;          // records of this generation are valid
   double wc_margin;         // a walk collects the leaves of B enlarged by this x B's half-extent
   double wc_loose;          // a record is reused only while vol(B+) <= this x vol(B)
+  int certify_prev;         // previous-match certificate mode (icp_hip_config.certify_prev)
 };
 
 // Threads per block of the per-thread search kernels for a given stack depth.
 int nn_block_threads(int levels);
 hipError_t launch_nn(const NNLaunch& a, hipStream_t s);
+// TgtPt::sep of every target point (lower bound of its distance to every other point).
+hipError_t launch_target_sep(const NodeRec* nodes, TgtPt* pts, int64_t n, int levels, hipStream_t s);
 
 // Residual moments of the settled queries in fixed parts (deterministic), then the merges.
 int64_t moments_num_parts(int64_t n);

@@ -31,6 +31,14 @@
 #ifndef ICP_SHRINK_RETRY
 #define ICP_SHRINK_RETRY 1
 #endif
+#ifndef ICP_SKIP_PREV_GATHER
+#define ICP_SKIP_PREV_GATHER 1
+#endif
+// Diagnostic build only (-DICP_WINNER_COUNTS=1): debug slots 20, 22, 23 count how often the fp32
+// winner is the previous match (its registers would otherwise cost the product build a spill).
+#ifndef ICP_WINNER_COUNTS
+#define ICP_WINNER_COUNTS 0
+#endif
 constexpr bool kDbgCounts = !ICP_PHASE_CLOCKS;  // the clock build counts nothing (no atomics)
 #if ICP_PHASE_CLOCKS
 #define PCLK(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
@@ -149,6 +157,17 @@ __device__ __forceinline__ double scan32_lower_bound(float s32, double ext) {
   return d * d * (1.0 - 0x1p-48);
 }
 
+// The certificate of the previous match p* (fl(d2) = u from the moved query, p*'s separation S):
+// every other point p has D(q', p) >= S - D* with D* <= sqrt(u) (1 + 2^-50), and
+// fl(d2(q', p)) >= D^2 (1 - 5 2^-53); so the window test of nn_device.h's certificate applies
+// with the lower bound (S - D*)^2 (1 - 2^-50) (its rounding covered by the 2^-52 / 2^-50 factors).
+__device__ __forceinline__ bool prev_certified(double u, float sep, double init_best) {
+  const double dstar = __builtin_sqrt(u) * (1.0 + 0x1p-50);
+  const double g = ((double)sep - dstar) * (1.0 - 0x1p-52);
+  if (!(g > 0.0)) return false;
+  return certified(u, g * g * (1.0 - 0x1p-50), init_best);
+}
+
 // Workgroups are dispatched round-robin over the 8 XCDs (block b runs on XCD b % 8), each with
 // its own 4 MB L2. Renumbered, XCD x takes runs of C consecutive logical blocks (C = chunk), the
 // runs dealt round-robin over the XCDs: the waves an XCD runs at a time are neighbours in the kd
@@ -193,13 +212,21 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
   PCLK(t_p0);
   // Phase 1: the guess (any value is safe: certification also requires best <= u).
   double u = __builtin_inf();
+  int32_t prev_pos = -1;  // the previous match (leaf order), whose fl(d2) is u
+  bool safe = false;      // the previous match certified from its separation: no search
   if (active && finite_q && a.have_prev) {
     // the previous match is a candidate: its fl(d2) from the moved query bounds the nearest
     // point's (usually well below (previous residual + displacement)^2)
-    const TgtPt* pp = a.pts + a.pos_out[i];
+    prev_pos = a.pos_out[i];
+    const TgtPt* pp = a.pts + prev_pos;
     const double2 pxy = *reinterpret_cast<const double2*>(&pp->x);
-    const double dx = pxy.x - qx, dy = pxy.y - qy, dz = pp->z - qz;
+    const double2 pzs = *reinterpret_cast<const double2*>(&pp->z);  // z, (orig, sep)
+    const double dx = pxy.x - qx, dy = pxy.y - qy, dz = pzs.x - qz;
     u = dx * dx + dy * dy + dz * dz;
+    if (a.certify_prev) {
+      const float sep = __int_as_float((int)((unsigned long long)__double_as_longlong(pzs.y) >> 32));
+      safe = prev_certified(u, sep, a.init_best);
+    }
   } else if (active && finite_q) {
     const NodeRec* r0 = a.nodes;
     double lx = r0->lo[0], ly = r0->lo[1], lz = r0->lo[2], hx = r0->hi[0], hy = r0->hi[1], hz = r0->hi[2];
@@ -241,6 +268,32 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
     }
   }
 
+  // Phase 1b (icp_hip_config.certify_prev): lanes whose previous match is certified are settled
+  // (their match position stays; the residual is sqrt(u), computeDistance bit for bit).
+  //   1: a wave whose active lanes are all certified ends here; other waves search every lane
+  //   2: certified lanes settle, the others search (join) as usual
+  //   3: certified lanes settle, the others go to the ball search (with u as their guess): every
+  //      wave ends here
+  if (a.certify_prev && a.have_prev) {
+    const unsigned long long open = __ballot(active && !safe);
+    if (kDbgCounts && a.dbg && lane == 0) {
+      atomicAdd(&a.dbg[19], (unsigned long long)__popcll(__ballot(safe)));
+      if (open == 0) atomicAdd(&a.dbg[18], 1ull);
+    }
+    if (open == 0 || a.certify_prev == 3) {
+      if (safe) a.dist_out[i] = __builtin_sqrt(u);
+      if (open != 0) {
+        if (active && !finite_q) {
+          a.pos_out[i] = a.pos0;
+          a.dist_out[i] = residual_to(a.pts, a.pos0, qx, qy, qz);
+        }
+        wave_append_u(active && finite_q && !safe, i, u, a.fb_count + 1, a.fb_list2, a.fb_u2);
+      }
+      return;
+    }
+    if (a.certify_prev == 1) safe = false;  // the whole wave searches
+  }
+
   PCLK(t_p1);
   // Phase 2: the wave's search box over the lanes that join. Every point with fl(d2) <= u (1 +
   // 2^-47) lies within r of the query, r >= sqrt(u) (1 + 2^-40) + |q|_max 2^-45 (ball_radius32).
@@ -248,7 +301,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
   // joined query o, rounded outwards, and converted back to fp64 rounded outwards.
   const double amax = __builtin_fmax(__builtin_fabs(qx), __builtin_fmax(__builtin_fabs(qy), __builtin_fabs(qz)));
   // |q| <= 2^100 keeps every fp32 offset of the wave finite
-  const bool cand = active && finite_q && u <= 0x1p900 && amax <= 0x1p100;
+  const bool cand = active && finite_q && !safe && u <= 0x1p900 && amax <= 0x1p100;
   const float r = cand ? ball_radius32(u, amax) : 0.f;
   const unsigned long long cmask = __ballot(cand);
   // the join rule is a heuristic (any subset may join): fp32 mean
@@ -689,10 +742,23 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
       const float s2 = __uint_as_float(__float_as_uint(k2) & ~63u);  // <= the second-smallest value
       // fp64 distance of the fp32 winner, exactly as the leaf scan computes it (octree.cpp:139-144)
       double b64 = __builtin_inf();
-      if (join && p1 >= 0) {
+      if (ICP_SKIP_PREV_GATHER && join && p1 >= 0 && p1 == prev_pos) {
+        // the winner is the previous match: the guess evaluated exactly this expression on the
+        // same operands (moved query, same target record), so u is its fl(d2) bit for bit
+        b64 = u;
+      } else if (join && p1 >= 0) {
         const TgtPt* p = a.pts + p1;
         const double dx = p->x - qx, dy = p->y - qy, dz = p->z - qz;
         b64 = dx * dx + dy * dy + dz * dz;
+      }
+      if (ICP_WINNER_COUNTS && a.dbg) {
+        const unsigned long long same = __ballot(join && p1 >= 0 && p1 == prev_pos);
+        const unsigned long long won = __ballot(join && p1 >= 0);
+        if (lane == 0) {
+          atomicAdd(&a.dbg[22], (unsigned long long)__popcll(same));
+          atomicAdd(&a.dbg[23], (unsigned long long)__popcll(won));
+          if (won != 0 && (won & ~same) == 0) atomicAdd(&a.dbg[20], 1ull);
+        }
       }
       const double lb2 = scan32_lower_bound(s2, ext * (1.0 + 0x1p-19));
       // Decided lanes: nothing scanned; every point beyond the guess (the fp32 winner and the
@@ -793,7 +859,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
   if (kDbgCounts && a.dbg) {
     const unsigned long long ex = __ballot(cand && !join && !overflow);
     const unsigned long long cov = __ballot(join && !(best <= u));
-    const unsigned long long nc = __ballot(active && finite_q && !cand);
+    const unsigned long long nc = __ballot(active && finite_q && !safe && !cand);
     if (lane == 0) {
       atomicAdd(&a.dbg[2], (unsigned long long)__popcll(ex));
       atomicAdd(&a.dbg[3], (unsigned long long)__popcll(cov));
@@ -807,7 +873,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
   bool written = false, to_exact = false, to_lane = false;
   double d = 0.0;
   int32_t pos = bpos;
-  if (active) {
+  if (safe) {
+    a.dist_out[i] = __builtin_sqrt(u);  // settled in phase 1b (the position stays)
+  } else if (active) {
     if (!finite_q) {
       // NaN: every leaf distance is NaN; inf: the root's distance is inf. Either way the
       // reference keeps findNearest's default index 0 (octree.cpp:179).
@@ -1041,6 +1109,127 @@ __global__ void __launch_bounds__(64) k_nn_ball(NNLaunch a) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Separation of the target points (once per target): for every point p_j a lower bound S_j of its
+// exact distance to every OTHER target point, stored in TgtPt::sep (fp32, rounded down; 0 when
+// p_j has an exact duplicate). It turns the previous match into a certificate (k_nn_wave,
+// icp_hip_config.certify_prev): a moved query q' with exact distance D* to its previous match p*
+// has D(q', p) >= S - D* for every other point p (triangle inequality), so p* is the nearest with
+// the reference's own certificate (nn_device.h) whenever (S - D*)^2 clears fl(d2(q', p*)) by the
+// window. One thread per point (leaf order: neighbours in flight together), a branch-and-bound
+// DFS for the nearest point other than itself: nearest child first, the remaining siblings of a
+// level kept as one stack entry with a 16-bit lower-bound key (fast_dfs's encoding); a node is
+// skipped when its squared box distance s exceeds the best (monotone rounding: every point inside
+// has fl(d2) >= s), so the result is the exact minimum fl(d2) over the other points.
+__global__ void __launch_bounds__(256) k_target_sep(const NodeRec* __restrict__ nodes, TgtPt* __restrict__ pts,
+                                                    int64_t n) {
+  extern __shared__ __attribute__((aligned(16))) unsigned long long sep_stack[];
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;  // no barriers below
+  unsigned long long* st = sep_stack + threadIdx.x;
+  const int bs = blockDim.x;
+  const double2 qxy = *reinterpret_cast<const double2*>(&pts[j].x);
+  const double qx = qxy.x, qy = qxy.y, qz = pts[j].z;
+  double best = __builtin_inf();
+  uint32_t thr_key = key16(best);
+  int sp = 0;
+  int32_t node = 0;
+  double lx = nodes[0].lo[0], ly = nodes[0].lo[1], lz = nodes[0].lo[2];
+  double hx = nodes[0].hi[0], hy = nodes[0].hi[1], hz = nodes[0].hi[2];
+  double s = box_s(lx, ly, lz, hx, hy, hz, qx, qy, qz);
+  while (true) {
+    bool entered = false;
+    if (!(s > best)) {
+      const int2 topo = *reinterpret_cast<const int2*>(&nodes[node].first);
+      const int32_t first = topo.x;
+      const uint32_t meta = (uint32_t)topo.y;
+      if (meta & kLeafBit) {
+        const int32_t cnt = (int32_t)(meta & ~kLeafBit);
+        for (int32_t k = 0; k < cnt; k++) {
+          if ((int64_t)first + k == j) continue;
+          const TgtPt* p = pts + first + k;
+          const double2 pxy = *reinterpret_cast<const double2*>(&p->x);
+          const double dx = pxy.x - qx, dy = pxy.y - qy, dz = p->z - qz;
+          const double d2 = dx * dx + dy * dy + dz * dz;
+          if (d2 < best) {
+            best = d2;
+            thr_key = key16(best);
+          }
+        }
+      } else {
+        const double mx = (lx + hx) / 2, my = (ly + hy) / 2, mz = (lz + hz) / 2;
+        const double ax0 = smax(0.0, smax(lx - qx, qx - mx)), ax1 = smax(0.0, smax(mx - qx, qx - hx));
+        const double ay0 = smax(0.0, smax(ly - qy, qy - my)), ay1 = smax(0.0, smax(my - qy, qy - hy));
+        const double az0 = smax(0.0, smax(lz - qz, qz - mz)), az1 = smax(0.0, smax(mz - qz, qz - hz));
+        const double sx[2] = {ax0 * ax0, ax1 * ax1};
+        const double sy[2] = {ay0 * ay0, ay1 * ay1};
+        const double sz[2] = {az0 * az0, az1 * az1};
+        const uint32_t mask = meta & 0xffu;
+        double bs_ = __builtin_inf();
+        uint32_t o1 = 0;
+#pragma unroll
+        for (int o = 0; o < 8; o++) {
+          const double c = sx[o & 1] + sy[(o >> 1) & 1] + sz[o >> 2];
+          const bool take = ((mask >> o) & 1u) && c < bs_;
+          bs_ = take ? c : bs_;
+          o1 = take ? (uint32_t)o : o1;
+        }
+        const uint32_t rem = mask & ~(1u << o1);
+        uint32_t kmin = 0xffffu;
+#pragma unroll
+        for (int o = 0; o < 8; o++) {
+          const double c = sx[o & 1] + sy[(o >> 1) & 1] + sz[o >> 2];
+          const uint32_t kk = key16(c);
+          kmin = ((rem >> o) & 1u) && kk < kmin ? kk : kmin;
+        }
+        if (rem) {
+          st[sp * bs] = ((unsigned long long)kmin << 48) | ((unsigned long long)mask << 40) |
+                        ((unsigned long long)rem << 32) | (uint32_t)first;
+          sp++;
+        }
+        node = first + __builtin_popcount(mask & ((1u << o1) - 1u));
+        if (o1 & 1u) lx = mx; else hx = mx;
+        if (o1 & 2u) ly = my; else hy = my;
+        if (o1 & 4u) lz = mz; else hz = mz;
+        s = bs_;
+        entered = true;
+      }
+    }
+    if (entered) continue;
+    bool found = false;
+    while (sp > 0) {
+      const unsigned long long e = st[(sp - 1) * bs];
+      if ((uint32_t)(e >> 48) > thr_key) {  // key16 is monotone: every remaining child has s > best
+        sp--;
+        continue;
+      }
+      uint32_t rem = (uint32_t)(e >> 32) & 0xffu;
+      const uint32_t pmask = (uint32_t)(e >> 40) & 0xffu;
+      const int32_t first = (int32_t)(uint32_t)e;
+      const uint32_t o = (uint32_t)__builtin_ctz(rem);
+      rem &= rem - 1u;
+      if (rem == 0) sp--;
+      else st[(sp - 1) * bs] = (e & ~(0xffull << 32)) | ((unsigned long long)rem << 32);
+      node = first + __builtin_popcount(pmask & ((1u << o) - 1u));
+      const NodeRec* r = nodes + node;
+      const double2 l01 = *reinterpret_cast<const double2*>(&r->lo[0]);
+      const double2 l2h0 = *reinterpret_cast<const double2*>(&r->lo[2]);
+      const double2 h12 = *reinterpret_cast<const double2*>(&r->hi[1]);
+      lx = l01.x; ly = l01.y; lz = l2h0.x; hx = l2h0.y; hy = h12.x; hz = h12.y;
+      s = box_s(lx, ly, lz, hx, hy, hz, qx, qy, qz);
+      found = true;
+      break;
+    }
+    if (!found) break;
+  }
+  // fl(d2) <= D^2 (1 + 5 2^-53), so D >= sqrt(best) (1 - 2^-50) (the fp64 sqrt within an ulp);
+  // the fp32 conversion rounds by <= 2^-24, covered by the 2^-22 factor: sep <= D
+  float sep = __builtin_inff();
+  if (best < __builtin_inf()) sep = (float)(__builtin_sqrt(best) * ((1.0 - 0x1p-50) * (1.0 - 0x1p-22)));
+  if (!(sep >= 0.0f)) sep = 0.0f;
+  pts[j].sep = sep;
+}
+
 inline unsigned grid_for(int64_t n, int bs) { return (unsigned)((n + bs - 1) / bs); }
 
 }  // namespace
@@ -1050,6 +1239,15 @@ int nn_block_threads(int levels) {
   if (levels <= 32) return 256;
   if (levels <= 64) return 128;
   return 64;
+}
+
+hipError_t launch_target_sep(const NodeRec* nodes, TgtPt* pts, int64_t n, int levels, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  const int lv = levels < 1 ? 1 : levels;
+  const int bs = nn_block_threads(lv);
+  const size_t shmem = (size_t)lv * bs * sizeof(unsigned long long);
+  hipLaunchKernelGGL(k_target_sep, dim3(grid_for(n, bs)), dim3(bs), shmem, s, nodes, pts, n);
+  return hipGetLastError();
 }
 
 hipError_t launch_nn(const NNLaunch& a, hipStream_t s) {

@@ -30,7 +30,7 @@ struct Builder {
       p.y = xyz[3 * (int64_t)id + 1];
       p.z = xyz[3 * (int64_t)id + 2];
       p.orig = id;
-      p.pad = 0;
+      p.sep = 0.f;
       if (id == 0) out->pos_of_orig0 = (int32_t)out->pts.size();
       out->pts.push_back(p);
     }

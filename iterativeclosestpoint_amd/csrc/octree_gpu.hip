@@ -324,7 +324,7 @@ __global__ void __launch_bounds__(kTB) k_write_points(const double* __restrict__
   p.y = xyz[3 * (int64_t)o + 1];
   p.z = xyz[3 * (int64_t)o + 2];
   p.orig = o;
-  p.pad = 0;
+  p.sep = 0.f;
   pts[j] = p;
 }
 

@@ -44,3 +44,15 @@ def test_no_gpu_fails_loudly(icp):
         pytest.skip("a GPU is present")
     with pytest.raises(icp.IcpError):
         icp.Context(0)
+
+
+def test_create_multi_rejects_bad_arguments_without_a_gpu(icp):
+    """icp_hip_create_multi validates its device list and transport before touching a device."""
+    import ctypes as C
+    L = icp.lib()
+    h = C.c_void_p()
+    two = (C.c_int32 * 2)(0, 0)
+    assert L.icp_hip_create_multi(C.byref(h), 2, two, None, icp.XPORT_RCCL) == -1  # RCCL: distinct GPUs
+    assert L.icp_hip_create_multi(C.byref(h), 2, two, None, 7) == -1              # unknown transport
+    assert L.icp_hip_create_multi(C.byref(h), 0, two, None, icp.XPORT_AUTO) == -1  # empty list
+    assert not h.value

@@ -1,0 +1,142 @@
+"""One process driving several devices (icp_hip_create_multi; SURVEY.md §8(b) icp_hip_create(ctx,
+n_devices, device_ids)): the multi-GPU path behind the single-process drop-in
+(ICPEngine::registerPointClouds, icpengine.cpp:24-60; ICP(), icp_registration.cpp:443-446).
+
+The one-GPU box runs it two ways:
+  * N members on the same device (the in-process host gather: RCCL refuses two ranks on one
+    device), every member with its own driver thread, spatial shard and octree replica: the same
+    code path as N GPUs except the transport. Checked against a plain one-device run: every
+    iteration's statistics and transform to 1e-12 (merge order only), correspondences bit for bit
+    in the caller's order.
+  * devices = {0} over RCCL (ncclCommInitAll of one device, ncclAllGather on the member's
+    stream, rank-order device merges): bit-identical to the plain run.
+And the drop-in entry points with a device list: icp_engine_register_devices, icp_cli_icp_devices,
+the CLI's --devices.
+"""
+import subprocess
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = Path(__file__).resolve().parents[1]
+N = 300_000
+ITERS = 5
+
+
+def _run(icp, ctx, tgt, src):
+    ctx.set_target(tgt, 10, 20, icp.RULES_ENGINE)
+    ctx.set_source(src)
+    sess = ctx.session(icp.params_default(max_iterations=ITERS, tolerance=0.0))
+    recs, corr = [], []
+    for _ in range(ITERS):
+        r = sess.step()
+        recs.append((r.valid_points, r.rmse, r.mean, r.std, r.threshold, np.array(r.transform[:])))
+        corr.append(ctx.get_correspondences())
+    rc, res = sess.finish()
+    sess.close()
+    assert rc == 0 and res.success
+    return recs, corr, ctx.get_source()
+
+
+@pytest.fixture(scope="module")
+def pair(icp):
+    tgt, src, _ = icp.synth_pair(N, yaw_deg=3.0)
+    return tgt, src
+
+
+@pytest.fixture(scope="module")
+def plain(icp, pair):
+    with icp.Context(0) as ctx:
+        return _run(icp, ctx, *pair)
+
+
+@pytest.mark.parametrize("members", [2, 3, 8])
+def test_group_host_gather_matches_plain(icp, pair, plain, members):
+    with icp.Context(devices=[0] * members) as ctx:
+        ids, transport = ctx.devices()
+        assert ids == [0] * members and transport == icp.XPORT_HOST
+        recs, corr, moved = _run(icp, ctx, *pair)
+        # an iterate's search paths are summed over the members
+        st = ctx.iterate(None, ITERS, icp.RULES_ENGINE, 3.0)
+        assert st.n == N
+    p_recs, p_corr, p_moved = plain
+    for (v, rmse, mean, sd, thr, T), (pv, prmse, pmean, psd, pthr, pT) in zip(recs, p_recs):
+        assert v == pv
+        np.testing.assert_allclose([rmse, mean, sd, thr], [prmse, pmean, psd, pthr], rtol=1e-12)
+        np.testing.assert_allclose(T, pT, rtol=0, atol=1e-12)
+    # the first iterate searches the unmoved source: identical correspondences and residuals
+    np.testing.assert_array_equal(corr[0][0], p_corr[0][0])
+    np.testing.assert_array_equal(corr[0][1], p_corr[0][1])
+    # later ones searched sources moved by transforms equal to 1e-12: indices equal
+    for (idx, _), (pidx, _) in zip(corr, p_corr):
+        assert np.count_nonzero(idx != pidx) <= 1e-5 * N
+    np.testing.assert_allclose(moved, p_moved, rtol=0, atol=1e-9)
+
+
+def test_group_rccl_one_device_bit_identical(icp, pair, plain):
+    with icp.Context(devices=[0], transport=icp.XPORT_RCCL) as ctx:
+        ids, transport = ctx.devices()
+        assert ids == [0] and transport == icp.XPORT_RCCL
+        recs, corr, moved = _run(icp, ctx, *pair)
+    p_recs, p_corr, p_moved = plain
+    for a, b in zip(recs, p_recs):
+        assert a[:5] == b[:5]
+        np.testing.assert_array_equal(a[5], b[5])
+    for (idx, d), (pidx, pd) in zip(corr, p_corr):
+        np.testing.assert_array_equal(idx, pidx)
+        np.testing.assert_array_equal(d, pd)
+    np.testing.assert_array_equal(moved, p_moved)
+
+
+def test_group_argument_errors(icp, pair):
+    tgt, src = pair
+    with pytest.raises(icp.IcpError):
+        icp.Context(devices=[0, 0], transport=icp.XPORT_RCCL)  # RCCL: one rank per GPU
+    with icp.Context(devices=[0, 0, 0]) as ctx:
+        ctx.set_target(tgt, 10, 20, icp.RULES_ENGINE)
+        with pytest.raises(icp.IcpError):
+            ctx.set_source(src[:2])  # fewer points than devices
+        with pytest.raises(icp.IcpError):
+            ctx.comm_init_host(2, 0, lambda local: np.stack([local, local]))
+
+
+def test_engine_and_cli_with_device_lists(icp, pair):
+    tgt, src = pair
+    p = icp.params_default(max_iterations=20, tolerance=1e-9)
+    rc1, res1, hist1, out1 = icp.engine_register(p, src, tgt, devices=[0])
+    rc2, res2, hist2, out2 = icp.engine_register(p, src, tgt, devices=[0, 0, 0, 0])
+    assert rc1 == 0 and rc2 == 0 and res1.success and res2.success
+    assert res1.total_iterations == res2.total_iterations
+    assert [h.valid_points for h in hist1] == [h.valid_points for h in hist2]
+    np.testing.assert_allclose(np.array(res2.final_R), np.array(res1.final_R), atol=1e-12)
+    np.testing.assert_allclose(np.array(res2.final_t), np.array(res1.final_t), atol=1e-12)
+    np.testing.assert_allclose(out2, out1, atol=1e-9)
+    R1, t1, tr1, s1 = icp.cli_icp(src, tgt, 10, 1e-2, devices=[0])
+    R2, t2, tr2, s2 = icp.cli_icp(src, tgt, 10, 1e-2, devices=[0, 0])
+    assert len(tr1) == len(tr2)
+    np.testing.assert_allclose(R2, R1, atol=1e-12)
+    np.testing.assert_allclose(t2, t1, atol=1e-12)
+
+
+def test_cli_binary_devices_flag(icp, pair, tmp_path):
+    tgt, src = pair
+    cli = ROOT / "iterativeclosestpoint_amd" / "bin" / "icp_registration"
+    if not cli.exists():
+        pytest.skip("CLI binary not built")
+    icp.las_write_cli(tmp_path / "Scan_096_origin.las", src[:100000])
+    icp.las_write_cli(tmp_path / "Scannew_099.las", tgt[:100000])
+    outs = {}
+    for tag, flag in (("one", ["--device", "0"]), ("two", ["--devices", "0,0"])):
+        d = tmp_path / tag
+        d.mkdir()
+        r = subprocess.run([str(cli), "--source", str(tmp_path / "Scan_096_origin.las"), "--target",
+                            str(tmp_path / "Scannew_099.las"), "--sample-rate", "5", "--outdir", str(d)] + flag,
+                           capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, r.stdout + r.stderr
+        outs[tag] = (r.stdout, (d / "icp_transformation.txt").read_text())
+    assert "devices: 2 GPUs" in outs["two"][0] and "devices:" not in outs["one"][0]
+    # same report shape (one block per cumulative transform)
+    assert len(outs["one"][1].splitlines()) == len(outs["two"][1].splitlines())

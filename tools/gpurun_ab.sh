@@ -21,7 +21,7 @@ for r in $(seq 1 $REPS); do
     if [ "$ARM" != "$L" ]; then for kv in $(echo "${ARM#*:}" | tr ',' ' '); do CF="$CF --config $kv"; done; fi
     if [ "$L" = "cur" ]; then unset ICP_HIP_LIB; else export ICP_HIP_LIB=$PWD/$L; fi
     OUTF=gpurun_out/ab_$TAG.$r.$a.json
-    timeout -k 10 300 python3 bench.py --no-cpu-baseline --no-parity $CF > $OUTF 2> gpurun_out/ab_$TAG.err || { tail -20 gpurun_out/ab_$TAG.err; exit 1; }
+    timeout -k 10 300 python3 bench.py --no-cpu-baseline --no-parity --no-registration $CF > $OUTF 2> gpurun_out/ab_$TAG.err || { tail -20 gpurun_out/ab_$TAG.err; exit 1; }
     python3 -c "
 import json,sys; j=json.load(open(sys.argv[1])); r=j['roofline'] or {}
 print(f\"{sys.argv[2]:48s} value {j['value']:9.1f} median {j['median']['value']:9.1f} k_nn_wave {r.get('kernel_ms_avg')} ms iter_dev {r.get('iterate_device_ms_avg')} ball {j['search_paths']['ball']} lane {j['search_paths']['lane']} exact {j['search_paths']['exact_fallback']}\")" $OUTF "$ARM"

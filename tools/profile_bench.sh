@@ -8,7 +8,7 @@ REPO=$(pwd)
 OUT=$REPO/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-BENCH="$REPO/bench.py --points $N --no-cpu-baseline --no-parity"
+BENCH="$REPO/bench.py --points $N --no-cpu-baseline --no-parity --no-registration"
 cd /tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o "$TAG" -- \
   python3 $BENCH --steps 200 --warmup 5 > "$OUT/bench_traced.json" 2> "$OUT/trace.err" || exit $?
