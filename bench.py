@@ -19,8 +19,8 @@ iterations (max over ranks); `median` = the same rate from the median iteration 
                 64 B per query streamed + every target point (28 B) and node (56 B) once) / its
                 average HIP-event duration over the timed iterations; `traffic` = PMC bytes per
                 launch (rocprofv3, calibrated per access width: tools/calib_pmc.sh) of the same
-                kernel source, or null; `traffic_gbs` / `traffic_frac` = those bytes over this
-                run's kernel time, against the peak.
+                kernel source, or null; `fabric_gbs` = those bytes over this run's kernel time
+                (L2 -> fabric requests, Infinity-Cache hits included: not an HBM rate).
   reference_work  SURVEY.md §8d's model of the reference DFS's work (148 + 56 V + 24 P bytes per
                 correspondence): what the reference would move, not what this kernel moves.
   cpu_baseline  the REFERENCE CPU path (oracle/_ref/ref_bench: icp_registration.cpp's ICP()),
@@ -323,7 +323,11 @@ def main() -> int:
         kv = dict(c.split("=", 1) for c in args.config)
         conf = icp.config(**{k: (float(v) if "." in v else int(v)) for k, v in kv.items()})
     ctx = icp.Context(devices=[k % n_dev for k in range(args.gpus)], cfg=conf) if group else icp.Context(device, conf)
+    t_synth = time.perf_counter() - t_setup
+    t1 = time.perf_counter()
     ctx.set_target(tgt, 10, 20, icp.RULES_ENGINE)
+    t_target = time.perf_counter() - t1
+    t1 = time.perf_counter()
     # spatial shards: contiguous ranges of the kd order (a contiguous range of the shuffled cloud
     # would thin each rank's queries `world` times; see icp_host.h icp_source_shard_order)
     ctx.set_source(src[icp.source_shard_order(src)[lo:hi]] if world > 1 else src)
@@ -343,6 +347,7 @@ def main() -> int:
     elif args.rccl_self:
         with stdout_to_stderr():
             ctx.comm_init(1, 0, icp.Context.unique_id())
+    t_source = time.perf_counter() - t1
     setup_s = time.perf_counter() - t_setup
     build_on_dev, build_ms = ctx.target_build_info()
 
@@ -469,10 +474,10 @@ def main() -> int:
                 "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "traffic_over_algorithmic": None if traffic is None else round(traffic / need, 3),
-                # the PMC-measured HBM rate of the same launch (the profiled bytes over this run's
-                # kernel time) against the peak: the north star's "rocprof-measured GB/s"
-                "traffic_gbs": None if traffic is None else round(traffic / nn_avg_s / 1e9, 1),
-                "traffic_frac": None if traffic is None else round(traffic / nn_avg_s / 1e9 / HBM_PEAK_GBS, 4),
+                # the PMC bytes of the same launch over this run's kernel time: L2 -> fabric
+                # requests, which include Infinity-Cache (MALL) hits, so an upper bound of the HBM
+                # rate, not an HBM figure (`frac` above, compulsory bytes, is the roofline figure)
+                "fabric_gbs": None if traffic is None else round(traffic / nn_avg_s / 1e9, 1),
                 "kernel": "k_nn_wave<true> (fused transform + wave-cooperative certified octree NN + residual)",
                 "algorithmic_bytes_per_launch": round(need), "kernel_ms_avg": round(float(np.mean(nn_ms)), 4),
                 "iterate_device_ms_avg": round(float(np.mean(it_ms)), 4),
@@ -494,6 +499,10 @@ def main() -> int:
             "timed_state_parity": timed_parity,
             "registration": registration,
             "setup_s": round(setup_s, 2),
+            "setup": {"synthesis_s": round(t_synth, 3), "set_target_s": round(t_target, 3),
+                      "set_source_s": round(t_source, 3),
+                      "note": "host synthesis; set_target = upload + device octree build + tables; "
+                              "set_source = query order + upload (+ communicator setup for N > 1)"},
             "octree_build": {"on_device": build_on_dev, "ms": round(build_ms, 2)},
             "final_rmse": res.final_rmse,
         }

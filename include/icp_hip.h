@@ -83,8 +83,14 @@ typedef struct icp_hip_config {
                              a search (exact: the window certificate of DESIGN.md §3.1).
                              0: off; 1: only waves whose every query is certified skip the search;
                              2: certified queries settle, the rest of the wave searches;
-                             3: certified queries settle, the rest take the ball search   dflt 0 */
-  int32_t reserved[2];    /* zero */
+                             3: certified queries settle; a wave left with at most 4 open
+                                queries hands them to the ball search, else searches them (2).
+                             Pays off near convergence (residuals well below the point spacing);
+                             on config 4's sliding synthetic pair ~0.2 % of the queries certify
+                             and 1/2 cost +4 % search time          dflt 0 */
+  int32_t query_order;    /* the kd order of the source queries (64-query buckets = waves):
+                             0: built on the device; 1: on the host (query_order.cpp)  dflt 0 */
+  int32_t reserved[1];    /* zero */
 } icp_hip_config;
 
 /* Slots of icp_hip_debug_counters (summed over the last iterate's search launches). */

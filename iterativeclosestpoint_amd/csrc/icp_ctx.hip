@@ -164,6 +164,7 @@ int icp_hip_create_ex(icp_hip_ctx** out, int device, const icp_hip_config* cfg) 
   if (conf.candidate_cache != 0 && conf.candidate_cache != 1) return fail(ICP_HIP_EINVAL, "config: candidate_cache must be 0 or 1");
   if (conf.candidate_margin < 0 || conf.candidate_margin > 1024)
     return fail(ICP_HIP_EINVAL, "config: candidate_margin out of [0, 1024]");
+  if (conf.query_order != 0 && conf.query_order != 1) return fail(ICP_HIP_EINVAL, "config: query_order must be 0 or 1");
   if (conf.certify_prev < 0 || conf.certify_prev > 3) return fail(ICP_HIP_EINVAL, "config: certify_prev out of [0, 3]");
   if (!(conf.join_factor >= 1.0 && conf.join_factor <= 1e6))
     return fail(ICP_HIP_EINVAL, "config: join_factor out of [1, 1e6]");
@@ -389,9 +390,15 @@ int icp_hip_set_target(icp_hip_ctx* c, const double* xyz, int64_t n, int max_poi
   }
   if (c->cfg.cell_starts && c->n_nodes < ((int64_t)1 << 26)) {
     const int lmax = cell_table_depth(c->n_leaves, c->levels - 1);
-    HIP_TRY(dalloc(&c->cells, (size_t)cell_table_entries(lmax)));
-    HIP_TRY(build_cell_tables(c->nodes, lmax, c->cells, c->stream));
-    c->cell_lmax = lmax;
+    // the tables only speed up the searches' start: without memory for them the searches start
+    // from the root (identical results)
+    if (dalloc(&c->cells, (size_t)cell_table_entries(lmax)) == hipSuccess) {
+      HIP_TRY(build_cell_tables(c->nodes, lmax, c->cells, c->stream));
+      c->cell_lmax = lmax;
+    } else {
+      (void)hipGetLastError();
+      c->cells = nullptr;
+    }
   }
   HIP_TRY(hipEventRecord(e1, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
@@ -479,30 +486,36 @@ int icp_hip_set_source(icp_hip_ctx* c, const double* xyz, int64_t n) {
   HIP_TRY(dalloc(&c->fb_list, 3 * (size_t)n));
   HIP_TRY(dalloc(&c->fb_u, (size_t)n));
   if (c->cfg.candidate_cache && n > 0) {
+    // the cache only saves walks: without memory for it every iterate walks (identical results)
     const size_t nw = (size_t)((n + 63) / 64);
-    HIP_TRY(dalloc(&c->wc_box, nw));
-    HIP_TRY(dalloc(&c->wc_ents, nw * icp::kWaveCandCap));
-    HIP_TRY(hipMemsetAsync(c->wc_box, 0, nw * sizeof(icp::WaveBox), c->stream));  // generation 0: invalid
+    if (dalloc(&c->wc_box, nw) == hipSuccess && dalloc(&c->wc_ents, nw * icp::kWaveCandCap) == hipSuccess) {
+      HIP_TRY(hipMemsetAsync(c->wc_box, 0, nw * sizeof(icp::WaveBox), c->stream));  // generation 0: invalid
+    } else {
+      (void)hipGetLastError();
+      dfree(c->wc_box);
+      dfree(c->wc_ents);
+    }
   }
   c->wc_gen++;
   HIP_TRY(dalloc(&c->mparts, (size_t)(c->nb_mom + merge_scratch_entries(c->nb_mom))));
   HIP_TRY(dalloc(&c->cparts, (size_t)(c->nb_cull + merge_scratch_entries(c->nb_cull))));
   if (n == 0) return ICP_HIP_OK;
-  // Spatially compact query order (kd buckets of 64 = one wave), computed on the host.
-  std::vector<int32_t> perm;
-  kd_query_order(xyz, n, 8, &perm);
-  std::vector<double> reordered((size_t)(3 * n));
-  for (int64_t k = 0; k < n; k++) {
-    const double* p = xyz + 3 * (int64_t)perm[k];
-    reordered[3 * k] = p[0];
-    reordered[3 * k + 1] = p[1];
-    reordered[3 * k + 2] = p[2];
-  }
+  // Spatially compact query order (kd buckets of 64 = one wave): on the device from the uploaded
+  // cloud (query_order_gpu.hip), or on the host (config query_order = 1)
   double* aos = nullptr;
   hipError_t e = dalloc(&aos, 3 * (size_t)n);
-  if (e == hipSuccess) e = hipMemcpyAsync(aos, reordered.data(), 3 * sizeof(double) * n, hipMemcpyHostToDevice, c->stream);
-  if (e == hipSuccess) e = hipMemcpyAsync(c->perm, perm.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, c->stream);
-  if (e == hipSuccess) e = launch_deinterleave(aos, c->x, c->y, c->z, n, c->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(aos, xyz, 3 * sizeof(double) * n, hipMemcpyHostToDevice, c->stream);
+  if (e == hipSuccess) {
+    if (c->cfg.query_order == 0) {
+      e = gpu_kd_query_order(aos, n, 8, c->perm, c->stream);
+    } else {
+      std::vector<int32_t> perm;
+      kd_query_order(xyz, n, 8, &perm);
+      e = hipMemcpyAsync(c->perm, perm.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, c->stream);
+      if (e == hipSuccess) e = hipStreamSynchronize(c->stream);  // the host order is read by the copy
+    }
+  }
+  if (e == hipSuccess) e = launch_gather_deinterleave(aos, c->perm, c->x, c->y, c->z, n, c->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
   dfree(aos);
   if (e != hipSuccess) return fail(ICP_HIP_EDEVICE, std::string("set_source: ") + hipGetErrorString(e));

@@ -283,8 +283,28 @@ int group_set_source(icp_hip_ctx* c, const double* xyz, int64_t n) {
   DeviceGroup* g = c->group;
   const int w = (int)g->members.size();
   if (n < w) return fail(ICP_HIP_EINVAL, "set_source: a multi-device context needs at least one point per device");
-  // spatially compact shards: contiguous ranges of the kd order (icp_source_shard_order)
-  icp::kd_query_order(xyz, n, 8, &g->order);
+  // spatially compact shards: contiguous ranges of the kd order (icp_source_shard_order's order),
+  // built on the first device (or on the host: config query_order = 1, or no device memory)
+  g->order.assign((size_t)n, 0);
+  bool ordered = false;
+  if (c->cfg.query_order == 0) {
+    icp_hip_ctx* m0 = g->members[0];
+    double* d_xyz = nullptr;
+    int32_t* d_perm = nullptr;
+    hipError_t e = hipSetDevice(m0->device);
+    if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&d_xyz), 3 * sizeof(double) * (size_t)n);
+    if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&d_perm), sizeof(int32_t) * (size_t)n);
+    if (e == hipSuccess) e = hipMemcpyAsync(d_xyz, xyz, 3 * sizeof(double) * (size_t)n, hipMemcpyHostToDevice, m0->stream);
+    if (e == hipSuccess) e = icp::gpu_kd_query_order(d_xyz, n, 8, d_perm, m0->stream);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(g->order.data(), d_perm, sizeof(int32_t) * (size_t)n, hipMemcpyDeviceToHost, m0->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(m0->stream);
+    if (d_xyz) (void)hipFree(d_xyz);
+    if (d_perm) (void)hipFree(d_perm);
+    ordered = e == hipSuccess;
+    if (!ordered) (void)hipGetLastError();
+  }
+  if (!ordered) icp::kd_query_order(xyz, n, 8, &g->order);
   shard_ranges(n, w, &g->lo);
   g->n_src = n;
   return for_members(g, [&](int k, icp_hip_ctx* m) {

@@ -134,5 +134,7 @@ hipError_t launch_scatter_corr(const int32_t* perm, const int32_t* pos, const Tg
                                int32_t* idx_out, const double* dist_in, double* dist_out, int64_t n,
                                hipStream_t s);
 hipError_t launch_deinterleave(const double* aos, double* x, double* y, double* z, int64_t n, hipStream_t s);
+hipError_t launch_gather_deinterleave(const double* aos, const int32_t* perm, double* x, double* y, double* z,
+                                      int64_t n, hipStream_t s);
 
 }  // namespace icp

@@ -31,8 +31,13 @@
 #ifndef ICP_SHRINK_RETRY
 #define ICP_SHRINK_RETRY 1
 #endif
+// Staging layout of the fp32 scan for NG <= 2: each scan group's pairs contiguous (1) or the
+// groups interleaved (0)
+#ifndef ICP_STAGE_CONTIG
+#define ICP_STAGE_CONTIG 1
+#endif
 #ifndef ICP_SKIP_PREV_GATHER
-#define ICP_SKIP_PREV_GATHER 1
+#define ICP_SKIP_PREV_GATHER 0
 #endif
 // Diagnostic build only (-DICP_WINNER_COUNTS=1): debug slots 20, 22, 23 count how often the fp32
 // winner is the previous match (its registers would otherwise cost the product build a spill).
@@ -108,6 +113,7 @@ __global__ void __launch_bounds__(256) k_nn_ref(NNLaunch a) {
 // Each joined lane's ball lies in B, so every point within best (1 + 2^-48) of it was scanned:
 // the certificate of nn_device.h applies. Non-joined lanes go to the ball list, uncertified ones
 // to the exact list.
+constexpr int kOpenToBall = 4;   // certify_prev 3: open queries a wave hands to the ball search
 constexpr int kWaveQueue = 256;  // node ids of the walk's LIFO stack (staging area after the walk)
 constexpr int kWaveStartK = 2;   // start cells per lane (up to 128 start nodes per wave)
 constexpr int kWavePoints = 1024;  // candidate list area (up to kWaveCandCap ids)
@@ -182,7 +188,7 @@ __device__ __forceinline__ unsigned xcd_block(unsigned chunk) {
   return ((k / chunk) * 8u + x) * chunk + k % chunk;
 }
 
-template <bool APPLY, int NG>
+template <bool APPLY, int NG, bool CERT>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) k_nn_wave(NNLaunch a) {
   static_assert(NG == 1 || NG == 2 || NG == 4, "scan groups: 1, 2 or 4");
   extern __shared__ __attribute__((aligned(16))) unsigned long long lds_raw[];
@@ -220,13 +226,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
     prev_pos = a.pos_out[i];
     const TgtPt* pp = a.pts + prev_pos;
     const double2 pxy = *reinterpret_cast<const double2*>(&pp->x);
-    const double2 pzs = *reinterpret_cast<const double2*>(&pp->z);  // z, (orig, sep)
-    const double dx = pxy.x - qx, dy = pxy.y - qy, dz = pzs.x - qz;
+    const double dx = pxy.x - qx, dy = pxy.y - qy, dz = pp->z - qz;
     u = dx * dx + dy * dy + dz * dz;
-    if (a.certify_prev) {
-      const float sep = __int_as_float((int)((unsigned long long)__double_as_longlong(pzs.y) >> 32));
-      safe = prev_certified(u, sep, a.init_best);
-    }
+    if (CERT) safe = prev_certified(u, pp->sep, a.init_best);
   } else if (active && finite_q) {
     const NodeRec* r0 = a.nodes;
     double lx = r0->lo[0], ly = r0->lo[1], lz = r0->lo[2], hx = r0->hi[0], hy = r0->hi[1], hz = r0->hi[2];
@@ -272,15 +274,15 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
   // (their match position stays; the residual is sqrt(u), computeDistance bit for bit).
   //   1: a wave whose active lanes are all certified ends here; other waves search every lane
   //   2: certified lanes settle, the others search (join) as usual
-  //   3: certified lanes settle, the others go to the ball search (with u as their guess): every
-  //      wave ends here
-  if (a.certify_prev && a.have_prev) {
+  //   3: certified lanes settle; a wave left with at most kOpenToBall open queries sends them to
+  //      the ball search (with u as their guess) and ends here, otherwise it searches them (2)
+  if (CERT && a.have_prev) {
     const unsigned long long open = __ballot(active && !safe);
     if (kDbgCounts && a.dbg && lane == 0) {
       atomicAdd(&a.dbg[19], (unsigned long long)__popcll(__ballot(safe)));
       if (open == 0) atomicAdd(&a.dbg[18], 1ull);
     }
-    if (open == 0 || a.certify_prev == 3) {
+    if (open == 0 || (a.certify_prev == 3 && __popcll(open) <= kOpenToBall)) {
       if (safe) a.dist_out[i] = __builtin_sqrt(u);
       if (open != 0) {
         if (active && !finite_q) {
@@ -586,10 +588,15 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
         gh[g][2] = uni((ghi[g][2] + doz) + mg);
       }
       constexpr int S = 64 / NG;  // lanes of a group = points of a group's segment per round
+      constexpr int S_ = S;
       const int gq = lane / S;    // this lane's group
       // staging area: NG segments of S points, in pairs [x0 x1 y0 y1 z0 z1 w0 w1] (32 B) so that
-      // one packed fp32 instruction (v_pk_add/mul/fma_f32) evaluates an axis of two points; pair
-      // k of group g at (k NG + g): the groups' concurrent reads fall on distinct banks
+      // one packed fp32 instruction (v_pk_add/mul/fma_f32) evaluates an axis of two points.
+      // Pair k of group g: NG <= 2, at g S/2 + k (each group's pairs contiguous: a group's scattered
+      // stores, 32 lanes x 4 B, meet each bank at most twice, which ds_write_b32 absorbs; with the
+      // groups interleaved they met it 4 times); NG = 4, at k NG + g (the b128 read lane groups
+      // mix two scan groups, whose concurrent broadcast reads then fall on distinct banks)
+      auto blk = [](int k, int g) { return (NG == 4 || !ICP_STAGE_CONTIG) ? k * NG + g : g * (S_ / 2) + k; };
       float* stage32 = reinterpret_cast<float*>(wl);
       // Selection keys: the fp32 squared distance with its low 6 bits replaced by the point's slot
       // in the segment (v_bfi), so that the two smallest are kept by two med3 per point and the
@@ -621,7 +628,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
         sel(sq.x, sl);
         sel(sq.y, (uint32_t)__builtin_amdgcn_readfirstlane((int)(sl + 1u)));  // a scalar operand
       };
-      const v4i* st4 = reinterpret_cast<const v4i*>(stage32) + 2 * gq;  // this group's pair 0
+      const v4i* st4 = reinterpret_cast<const v4i*>(stage32) + 2 * blk(0, gq);  // this group's pair 0
+      constexpr int kStep = (NG == 4 || !ICP_STAGE_CONTIG) ? 2 * NG : 2;        // v4i per pair step
       // One chunk of 64 candidates (lane = candidate base + lane; offsets vx, vy, vz, id bits vw):
       // group membership, rank among the group's points of the chunk, and (first round) the store
       // into the group's segment; `next` issues the following chunk's loads once this one is
@@ -643,7 +651,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
             }
             const int j = mask_rank(mk) - r0;
             if (in && j >= 0 && j < S) {
-              float* sp = stage32 + 8 * ((j >> 1) * NG + g) + (j & 1);
+              float* sp = stage32 + 8 * blk(j >> 1, g) + (j & 1);
               sp[0] = vx;
               sp[2] = vy;
               sp[4] = vz;
@@ -671,7 +679,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
             for (int g = 1; g < NG; g++) c = pg == g ? cn[g] : c;
             c -= r0;
             if (pj >= c && pj < len) {
-              float* sp = stage32 + 8 * ((pj >> 1) * NG + pg) + (pj & 1);
+              float* sp = stage32 + 8 * blk(pj >> 1, pg) + (pj & 1);
               sp[0] = 0x1p62f;
               sp[2] = 0x1p62f;
               sp[4] = 0x1p62f;
@@ -688,11 +696,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
             atomicAdd(&a.dbg[11], 1ull);
           }
 #pragma unroll 1
-          for (int k = 0; k < mp; k++) eval2(st4[2 * NG * k], st4[2 * NG * k + 1], 2u * k);
+          for (int k = 0; k < mp; k++) eval2(st4[kStep * k], st4[kStep * k + 1], 2u * k);
           // the winner of this round, if it improved the lane's best: its index from its slot
           if (k1 != k1_in) {
             const uint32_t sl = __float_as_uint(k1) & 63u;
-            p1 = __float_as_int(stage32[8 * ((sl >> 1) * NG + gq) + 6 + (sl & 1u)]);
+            p1 = __float_as_int(stage32[8 * blk((int)(sl >> 1), gq) + 6 + (sl & 1u)]);
           }
         }
       };
@@ -1276,13 +1284,21 @@ hipError_t launch_nn(const NNLaunch& a, hipStream_t s) {
   auto wave = [&](auto kern) {
     hipExtLaunchKernelGGL(kern, dim3(wgrid), dim3(256), (uint32_t)wshm, s, a.ev_start, a.ev_fast_done, 0u, a);
   };
-  switch ((a.apply ? 8 : 0) + a.scan_groups) {
-    case 9: wave(k_nn_wave<true, 1>); break;
-    case 10: wave(k_nn_wave<true, 2>); break;
-    case 12: wave(k_nn_wave<true, 4>); break;
-    case 1: wave(k_nn_wave<false, 1>); break;
-    case 2: wave(k_nn_wave<false, 2>); break;
-    case 4: wave(k_nn_wave<false, 4>); break;
+  // the previous-match certificate only where it can apply (an iterate after a search)
+  const bool cert = a.certify_prev != 0 && a.have_prev;
+  switch ((cert ? 16 : 0) + (a.apply ? 8 : 0) + a.scan_groups) {
+    case 9: wave(k_nn_wave<true, 1, false>); break;
+    case 10: wave(k_nn_wave<true, 2, false>); break;
+    case 12: wave(k_nn_wave<true, 4, false>); break;
+    case 1: wave(k_nn_wave<false, 1, false>); break;
+    case 2: wave(k_nn_wave<false, 2, false>); break;
+    case 4: wave(k_nn_wave<false, 4, false>); break;
+    case 16 + 9: wave(k_nn_wave<true, 1, true>); break;
+    case 16 + 10: wave(k_nn_wave<true, 2, true>); break;
+    case 16 + 12: wave(k_nn_wave<true, 4, true>); break;
+    case 16 + 1: wave(k_nn_wave<false, 1, true>); break;
+    case 16 + 2: wave(k_nn_wave<false, 2, true>); break;
+    case 16 + 4: wave(k_nn_wave<false, 4, true>); break;
     default: return hipErrorInvalidValue;
   }
   // the follow-up lists are short (the ball list ~0.1 % of the queries, the exact list usually

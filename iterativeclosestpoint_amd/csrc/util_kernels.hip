@@ -49,9 +49,27 @@ __global__ void k_deinterleave(const double* aos, double* x, double* y, double* 
   z[i] = aos[3 * i + 2];
 }
 
+// x[k] = aos[perm[k]] (the kd-ordered SoA source from the caller's AoS cloud)
+__global__ void k_gather_deinterleave(const double* aos, const int32_t* perm, double* x, double* y, double* z,
+                                      int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t j = perm[i];
+  x[i] = aos[3 * j];
+  y[i] = aos[3 * j + 1];
+  z[i] = aos[3 * j + 2];
+}
+
 inline unsigned grid_for(int64_t n, int bs) { return (unsigned)((n + bs - 1) / bs); }
 
 }  // namespace
+
+hipError_t launch_gather_deinterleave(const double* aos, const int32_t* perm, double* x, double* y, double* z,
+                                      int64_t n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_gather_deinterleave, dim3(grid_for(n, 256)), dim3(256), 0, s, aos, perm, x, y, z, n);
+  return hipGetLastError();
+}
 
 hipError_t launch_apply(const double T[12], double* x, double* y, double* z, int64_t n, hipStream_t s) {
   if (n <= 0) return hipSuccess;

@@ -35,7 +35,11 @@ def test_separation_is_a_tight_lower_bound(icp):
 
 @pytest.mark.parametrize("mode", [1, 2, 3])
 def test_modes_equal_full_search_over_iterations(icp, oracle, mode):
-    tgt, src, _ = icp.synth_pair(1_000_000)
+    # an anisotropic cloud with a small known motion: the registration converges within a few
+    # iterates, residuals fall to the 1 mm noise, far below the point spacing (~5 cm), and most
+    # previous matches certify (config 4's yaw-symmetric pair keeps sliding: few do)
+    tgt, src, _ = icp.synth_pair(1_000_000, sigma=[8.0, 4.0, 1.5], yaw_deg=1.0, pitch_deg=0.5, roll_deg=-0.3,
+                                 t=[0.05, -0.03, 0.02])
 
     def run(conf):
         out, settled = [], []
@@ -59,7 +63,7 @@ def test_modes_equal_full_search_over_iterations(icp, oracle, mode):
         np.testing.assert_array_equal(da, db, err_msg=f"iterate {k}")
     np.testing.assert_array_equal(moved, moved2)
     # the certificate does the work once previous matches exist
-    assert max(settled[2:]) > 0.5 * len(src)
+    assert max(settled[2:]) > 0.5 * len(src), settled
     # the source as the last iterate searched it (the session's pending transform is not applied)
     oidx, od = oracle.OracleTree(tgt).nn(moved2, init_best=oracle.DBL_MAX)
     np.testing.assert_array_equal(got[-1][0], oidx)

@@ -262,7 +262,9 @@ def test_fallback_share_small_on_scans(icp, gpu_ctx):
                                    (1_000_000, {"scan_groups": 1}), (1_000_000, {"scan_groups": 4}),
                                    (300_000, {"xcd_blocks": 0}),
                                    (1_000_000, {"candidate_cache": 0}), (300_000, {"candidate_margin": 0}),
-                                   (300_000, {"candidate_margin": 256})])
+                                   (300_000, {"candidate_margin": 256}),
+                                   (1_000_000, {"query_order": 1}), (1_000_000, {"certify_prev": 3}),
+                                   (300_000, {"certify_prev": 2, "candidate_cache": 0})])
 def test_scan32_matches_fp64_scan(icp, n, cfg):
     """Every configuration of the certified search (fp32 filter scan vs fp64 scan, cell-table
     starts vs root descent, join rule, host-built octree) returns exactly the default's
