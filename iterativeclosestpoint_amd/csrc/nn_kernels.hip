@@ -31,10 +31,11 @@
 #ifndef ICP_SHRINK_RETRY
 #define ICP_SHRINK_RETRY 1
 #endif
-// Staging layout of the fp32 scan for NG <= 2: each scan group's pairs contiguous (1) or the
-// groups interleaved (0)
+// Staging layout of the fp32 scan for NG <= 2: each scan group's pairs contiguous (1: its
+// scattered stores meet a bank at most twice, but the layout costs two more spilled registers:
+// search 0.487-0.489 ms vs 0.478-0.481 at 10M, same box) or the groups interleaved (0, default)
 #ifndef ICP_STAGE_CONTIG
-#define ICP_STAGE_CONTIG 1
+#define ICP_STAGE_CONTIG 0
 #endif
 #ifndef ICP_SKIP_PREV_GATHER
 #define ICP_SKIP_PREV_GATHER 0

@@ -35,11 +35,11 @@ def test_separation_is_a_tight_lower_bound(icp):
 
 @pytest.mark.parametrize("mode", [1, 2, 3])
 def test_modes_equal_full_search_over_iterations(icp, oracle, mode):
-    # an anisotropic cloud with a small known motion: the registration converges within a few
-    # iterates, residuals fall to the 1 mm noise, far below the point spacing (~5 cm), and most
-    # previous matches certify (config 4's yaw-symmetric pair keeps sliding: few do)
-    tgt, src, _ = icp.synth_pair(1_000_000, sigma=[8.0, 4.0, 1.5], yaw_deg=1.0, pitch_deg=0.5, roll_deg=-0.3,
-                                 t=[0.05, -0.03, 0.02])
+    # a registration near convergence: an anisotropic cloud (spacing ~5 cm) moved by a few mm with
+    # 0.5 mm noise, so residuals stay far below the point spacing and most previous matches
+    # certify (config 4's yaw-symmetric pair keeps sliding by ~cm: ~0.2 % do)
+    tgt, src, _ = icp.synth_pair(1_000_000, sigma=[8.0, 4.0, 1.5], yaw_deg=0.02, pitch_deg=0.0, roll_deg=0.0,
+                                 t=[0.002, -0.001, 0.0005], noise_sigma=0.0005)
 
     def run(conf):
         out, settled = [], []
