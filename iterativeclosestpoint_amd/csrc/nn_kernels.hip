@@ -279,9 +279,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
   //      the ball search (with u as their guess) and ends here, otherwise it searches them (2)
   if (CERT && a.have_prev) {
     const unsigned long long open = __ballot(active && !safe);
-    if (kDbgCounts && a.dbg && lane == 0) {
-      atomicAdd(&a.dbg[19], (unsigned long long)__popcll(__ballot(safe)));
-      if (open == 0) atomicAdd(&a.dbg[18], 1ull);
+    if (kDbgCounts && a.dbg) {
+      const unsigned long long settled = __ballot(safe);  // every lane takes part in the ballot
+      if (lane == 0) {
+        atomicAdd(&a.dbg[19], (unsigned long long)__popcll(settled));
+        if (open == 0) atomicAdd(&a.dbg[18], 1ull);
+      }
     }
     if (open == 0 || (a.certify_prev == 3 && __popcll(open) <= kOpenToBall)) {
       if (safe) a.dist_out[i] = __builtin_sqrt(u);
