@@ -90,7 +90,10 @@ typedef struct icp_hip_config {
                              and 1/2 cost +4 % search time          dflt 0 */
   int32_t query_order;    /* the kd order of the source queries (64-query buckets = waves):
                              0: built on the device; 1: on the host (query_order.cpp)  dflt 0 */
-  int32_t reserved[1];    /* zero */
+  int32_t overflow_halves; /* 1: the queries of a wave whose search box overflows are searched
+                              again as two 32-query halves (k_nn_half) before the ball search;
+                              0: they go to the ball search                             dflt 1 */
+  int32_t reserved[4];    /* zero */
 } icp_hip_config;
 
 /* Slots of icp_hip_debug_counters (summed over the last iterate's search launches). */
@@ -110,6 +113,7 @@ typedef struct icp_hip_config {
 #define ICP_DBG_CACHE_STORES 13  /* waves that walked and stored their candidate list          */
 #define ICP_DBG_BALL_OVERFLOW 14 /* ball-search queries whose candidate set overflowed         */
 #define ICP_DBG_BALL_POINTS 15   /* points scanned by the ball search                          */
+#define ICP_DBG_HALVES 16        /* 32-query halves of overflowed waves searched again (k_nn_half) */
 #define ICP_DBG_CLK_GUESS 16     /* phase-clock build (-DICP_PHASE_CLOCKS=1), s_memtime: guess  */
 #define ICP_DBG_CLK_BOX 17       /*                          search box                        */
 #define ICP_DBG_CLK_WALK 18      /*                          walk (cells + batches)            */

@@ -30,7 +30,7 @@ DBG_NAMES = {0: "waves", 1: "overflow_waves", 2: "not_joined", 3: "not_covered",
              12: "cache_hits", 13: "cache_stores",
              5: "walk_batches", 6: "no_guess", 7: "candidates", 14: "ball_overflow", 15: "ball_points",
              21: "start_nodes", 20: "winner_prev_waves", 22: "winner_prev", 23: "winner_lanes",
-             18: "prev_cert_waves", 19: "prev_cert_lanes"}
+             18: "prev_cert_waves", 19: "prev_cert_lanes", 16: "halves"}
 
 _P = C.c_void_p
 _D = C.POINTER(C.c_double)
@@ -67,7 +67,7 @@ class HipConfig(C.Structure):
         ("octree_builder", C.c_int32), ("join_factor", C.c_double), ("debug_counters", C.c_int32),
         ("xcd_blocks", C.c_int32), ("scan_groups", C.c_int32), ("candidate_cache", C.c_int32),
         ("candidate_margin", C.c_int32), ("certify_prev", C.c_int32), ("query_order", C.c_int32),
-        ("reserved", C.c_int32 * 1),
+        ("overflow_halves", C.c_int32), ("reserved", C.c_int32 * 4),
     ]
 
 

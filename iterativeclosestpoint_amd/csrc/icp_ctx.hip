@@ -144,6 +144,7 @@ void icp_hip_config_default(icp_hip_config* cfg) {
   cfg->scan_groups = 2;
   cfg->candidate_cache = 1;
   cfg->candidate_margin = 16;
+  cfg->overflow_halves = 1;
 }
 
 int icp_hip_create(icp_hip_ctx** out, int device) { return icp_hip_create_ex(out, device, nullptr); }
@@ -164,6 +165,7 @@ int icp_hip_create_ex(icp_hip_ctx** out, int device, const icp_hip_config* cfg) 
   if (conf.candidate_cache != 0 && conf.candidate_cache != 1) return fail(ICP_HIP_EINVAL, "config: candidate_cache must be 0 or 1");
   if (conf.candidate_margin < 0 || conf.candidate_margin > 1024)
     return fail(ICP_HIP_EINVAL, "config: candidate_margin out of [0, 1024]");
+  if (conf.overflow_halves != 0 && conf.overflow_halves != 1) return fail(ICP_HIP_EINVAL, "config: overflow_halves must be 0 or 1");
   if (conf.query_order != 0 && conf.query_order != 1) return fail(ICP_HIP_EINVAL, "config: query_order must be 0 or 1");
   if (conf.certify_prev < 0 || conf.certify_prev > 3) return fail(ICP_HIP_EINVAL, "config: certify_prev out of [0, 3]");
   if (!(conf.join_factor >= 1.0 && conf.join_factor <= 1e6))
@@ -191,13 +193,13 @@ int icp_hip_create_ex(icp_hip_ctx** out, int device, const icp_hip_config* cfg) 
       hipHostMalloc(reinterpret_cast<void**>(&c->h_it), sizeof(IterDev), hipHostMallocMapped | hipHostMallocCoherent) !=
           hipSuccess ||
       hipHostGetDevicePointer(reinterpret_cast<void**>(&c->h_it_dev), c->h_it, 0) != hipSuccess ||
-      dalloc(&c->counters, 2) != hipSuccess || dalloc(&c->fb_count, 4) != hipSuccess ||
+      dalloc(&c->counters, 2) != hipSuccess || dalloc(&c->fb_count, 8) != hipSuccess ||
       (conf.debug_counters && dalloc(&c->dbg, ICP_DBG_SLOTS) != hipSuccess)) {
     icp_hip_destroy(c);
     return fail(ICP_HIP_ENOMEM, "context allocation failed");
   }
   (void)hipMemset(c->it, 0, sizeof(IterDev));
-  (void)hipMemset(c->fb_count, 0, 4 * sizeof(unsigned int));
+  (void)hipMemset(c->fb_count, 0, 8 * sizeof(unsigned int));
   if (c->dbg) (void)hipMemset(c->dbg, 0, ICP_DBG_SLOTS * sizeof(unsigned long long));
   std::memset(c->h_it, 0, sizeof(IterDev));
   c->lists_zero = true;
@@ -483,7 +485,7 @@ int icp_hip_set_source(icp_hip_ctx* c, const double* xyz, int64_t n) {
   HIP_TRY(dalloc(&c->perm, n));
   HIP_TRY(dalloc(&c->pos, n));
   HIP_TRY(dalloc(&c->dist, n));
-  HIP_TRY(dalloc(&c->fb_list, 3 * (size_t)n));
+  HIP_TRY(dalloc(&c->fb_list, 3 * (size_t)n + 64));  // exact, ball, (half, mask) pairs
   HIP_TRY(dalloc(&c->fb_u, (size_t)n));
   if (c->cfg.candidate_cache && n > 0) {
     // the cache only saves walks: without memory for it every iterate walks (identical results)
@@ -545,6 +547,7 @@ int icp_hip_iterate(icp_hip_ctx* c, const double* T_apply, int iter, int rules, 
     for (int k = 0; k < 12; k++) a.T[k] = T_apply[k];
   a.fb_list = c->fb_list;
   a.fb_list2 = c->fb_list + c->n_src;
+  a.fb_list3 = c->cfg.overflow_halves ? c->fb_list + 2 * c->n_src : nullptr;  // 2 (n/32 + 2) <= n + 64 ints
   a.fb_u2 = c->fb_u;
   a.fb_count = c->fb_count;
   a.have_prev = c->have_prev ? 1 : 0;
@@ -553,7 +556,7 @@ int icp_hip_iterate(icp_hip_ctx* c, const double* T_apply, int iter, int rules, 
   a.wc_gen = c->wc_gen;
   a.wc_margin = c->cfg.candidate_margin / 256.0;
   a.wc_loose = kCacheLoose;
-  if (!c->lists_zero) HIP_TRY(hipMemsetAsync(c->fb_count, 0, 4 * sizeof(unsigned int), s));
+  if (!c->lists_zero) HIP_TRY(hipMemsetAsync(c->fb_count, 0, 8 * sizeof(unsigned int), s));
   c->lists_zero = false;
   if (c->dbg) HIP_TRY(hipMemsetAsync(c->dbg, 0, ICP_DBG_SLOTS * sizeof(unsigned long long), s));
   a.ev_start = ev[0];
@@ -721,14 +724,15 @@ int icp_hip_nn(icp_hip_ctx* c, const double* q, int64_t n, int32_t* idx_out, dou
     a.n = n;
     int32_t* fbl = nullptr;
     double* fbu = nullptr;
-    if (e == hipSuccess) e = dalloc(&fbl, 3 * (size_t)n);
+    if (e == hipSuccess) e = dalloc(&fbl, 3 * (size_t)n + 64);
     if (e == hipSuccess) e = dalloc(&fbu, (size_t)n);
     a.fb_list = fbl;
     a.fb_list2 = fbl + n;
+    a.fb_list3 = c->cfg.overflow_halves ? fbl + 2 * n : nullptr;
     a.fb_u2 = fbu;
     a.fb_count = c->fb_count;
     unsigned int lists4[4] = {0, 0, 0, 0};
-    if (e == hipSuccess) e = hipMemsetAsync(c->fb_count, 0, 4 * sizeof(unsigned int), c->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(c->fb_count, 0, 8 * sizeof(unsigned int), c->stream);
     c->lists_zero = false;
     if (e == hipSuccess) e = launch_nn(a, c->stream);
     if (e == hipSuccess)

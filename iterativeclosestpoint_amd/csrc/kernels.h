@@ -57,7 +57,10 @@ struct NNLaunch {
   int32_t* fb_list2;        // queries a wave did not take -> ball search
   double* fb_u2;            // the distance guess u of each fb_list2 entry
   unsigned int* fb_count;   // [0] exact list, [1] ball list sizes; [2] per-lane searches, [3] DFS
-                            // finishes of the ball search (counts); zero at the launch
+                            // finishes of the ball search (counts); [4] half list size; zero at
+                            // the launch
+  int32_t* fb_list3;        // 32-query halves of overflowed waves, (half id, lane mask) pairs
+                            // (null: no half pass)
   hipEvent_t ev_start;      // optional: the main search kernel's start and end, recorded by its
   hipEvent_t ev_fast_done;  // own dispatch (hipExtLaunchKernel: no marker packets between kernels)
   int have_prev;            // dist_out holds the previous residuals of these queries

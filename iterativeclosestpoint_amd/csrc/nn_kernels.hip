@@ -189,14 +189,14 @@ __device__ __forceinline__ unsigned xcd_block(unsigned chunk) {
   return ((k / chunk) * 8u + x) * chunk + k % chunk;
 }
 
-template <bool APPLY, int NG, bool CERT>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) k_nn_wave(NNLaunch a) {
+// The search of one wave's queries (query i per lane; i >= n: an idle lane). HALF: the second
+// pass over the 32-query halves of the waves whose box overflowed (k_nn_half: queries already
+// moved, no candidate cache; lanes 32..63 idle).
+template <bool APPLY, int NG, bool CERT, bool HALF>
+__device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, const int lane, unsigned char* wl) {
   static_assert(NG == 1 || NG == 2 || NG == 4, "scan groups: 1, 2 or 4");
-  extern __shared__ __attribute__((aligned(16))) unsigned long long lds_raw[];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int32_t i = (int32_t)(xcd_block((unsigned)a.xcd_blocks) * blockDim.x + threadIdx.x);  // n <= INT32_MAX
+  static_assert(!(HALF && (APPLY || CERT)), "the half pass searches moved queries");
   const bool active = i < a.n;
-  unsigned char* wl = reinterpret_cast<unsigned char*>(lds_raw) + wv * kWaveLds;
   int32_t* queue = reinterpret_cast<int32_t*>(wl);
   double4* stage = reinterpret_cast<double4*>(wl);  // after the walk only
   int32_t* plist = queue + kWaveQueue;               // candidate points
@@ -208,7 +208,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
   // query: a reusing wave has its first chunk before the box is known (unused otherwise).
   const int32_t i0 = __builtin_amdgcn_readfirstlane(i);
   const uint32_t wid = (uint32_t)i0 >> 6;
-  const bool use_wc = a.wc_box != nullptr && i0 < a.n;
+  const bool use_wc = !HALF && a.wc_box != nullptr && i0 < a.n;
   double hdr = 0.0;
   float4 ent0 = make_float4(0.f, 0.f, 0.f, 0.f);
   if (use_wc) {
@@ -552,7 +552,32 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
     }
     if (kDbgCounts && a.dbg && lane == 0) atomicAdd(&a.dbg[13], 1ull);
   };
-  if (overflow) join = false;
+  // An overflowing wave (its box holds more candidates than the list takes): its joined queries
+  // are searched again as two 32-query halves (k_nn_half), each with the smaller box of its own
+  // balls; an overflowing half hands its queries to the ball search.
+  bool deferred = false;
+  if (overflow) {
+    if (!HALF && a.fb_list3 != nullptr) {
+      // entries (half id, mask of its deferred lanes): the half pass searches exactly these
+      const unsigned long long dm = __ballot(join);
+      deferred = join;
+      const unsigned nh = ((uint32_t)dm != 0u ? 1u : 0u) + ((dm >> 32) != 0ull ? 1u : 0u);
+      if (lane == 0 && nh > 0) {
+        unsigned at = atomicAdd(a.fb_count + 4, nh);
+        if ((uint32_t)dm != 0u) {
+          a.fb_list3[2 * at] = (int32_t)(2 * wid);
+          a.fb_list3[2 * at + 1] = (int32_t)(uint32_t)dm;
+          at++;
+        }
+        if ((dm >> 32) != 0ull) {
+          a.fb_list3[2 * at] = (int32_t)(2 * wid + 1);
+          a.fb_list3[2 * at + 1] = (int32_t)(uint32_t)(dm >> 32);
+        }
+        if (kDbgCounts && a.dbg) atomicAdd(&a.dbg[16], (unsigned long long)nh);
+      }
+    }
+    join = false;
+  }
   if (kDbgCounts && a.dbg && lane == 0) {
     atomicAdd(&a.dbg[0], 1ull);
     if (overflow) atomicAdd(&a.dbg[1], 1ull);
@@ -900,7 +925,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
       written = certified(best, second, a.init_best);
       to_exact = !written;
       d = __builtin_sqrt(best);
-    } else {
+    } else if (!deferred) {
       to_lane = true;
     }
     if (written) {
@@ -921,6 +946,33 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
     atomicAdd(&a.dbg[20], t_p5 - t_p4);
   }
 #endif
+}
+
+template <bool APPLY, int NG, bool CERT>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) k_nn_wave(NNLaunch a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned long long lds_raw[];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int32_t i = (int32_t)(xcd_block((unsigned)a.xcd_blocks) * blockDim.x + threadIdx.x);  // n <= INT32_MAX
+  wave_search<APPLY, NG, CERT, false>(a, i, lane, reinterpret_cast<unsigned char*>(lds_raw) + wv * kWaveLds);
+}
+
+// The half pass: every wave takes 32-query halves of overflowed waves from the list (grid-stride;
+// the list is complete when this kernel starts), lanes 0..31 each one query.
+template <int NG>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) k_nn_half(NNLaunch a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned long long lds_raw[];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  unsigned char* wl = reinterpret_cast<unsigned char*>(lds_raw) + wv * kWaveLds;
+  const unsigned cnt = a.fb_count[4];
+  const unsigned waves = gridDim.x * (blockDim.x >> 6);
+  for (unsigned j = blockIdx.x * (blockDim.x >> 6) + wv; j < cnt; j += waves) {
+    const int32_t hb = a.fb_list3[2 * j];
+    const uint32_t mask = (uint32_t)a.fb_list3[2 * j + 1];  // the lanes the first pass deferred
+    const int64_t q = (int64_t)hb * 32 + lane;
+    const int32_t i = (lane < 32 && ((mask >> lane) & 1u) && q < a.n) ? (int32_t)q : (int32_t)a.n;
+    wave_lds_fence();  // the previous half's LDS reads are done
+    wave_search<false, NG, false, true>(a, i, lane, wl);
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1304,6 +1356,22 @@ hipError_t launch_nn(const NNLaunch& a, hipStream_t s) {
     case 16 + 2: wave(k_nn_wave<false, 2, true>); break;
     case 16 + 4: wave(k_nn_wave<false, 4, true>); break;
     default: return hipErrorInvalidValue;
+  }
+  // the half pass over the overflowed waves (queries already moved: no transform, no cache)
+  if (a.fb_list3) {
+    NNLaunch h = a;
+    h.apply = 0;
+    h.wc_box = nullptr;
+    h.wc_ents = nullptr;
+    const int64_t halves = (a.n + 31) / 32;
+    const int64_t hb = (halves + 3) / 4;
+    const unsigned hgrid = (unsigned)(hb < 2048 ? hb : 2048);  // about one resident block per slot
+    switch (a.scan_groups) {
+      case 1: hipLaunchKernelGGL(k_nn_half<1>, dim3(hgrid), dim3(256), wshm, s, h); break;
+      case 2: hipLaunchKernelGGL(k_nn_half<2>, dim3(hgrid), dim3(256), wshm, s, h); break;
+      case 4: hipLaunchKernelGGL(k_nn_half<4>, dim3(hgrid), dim3(256), wshm, s, h); break;
+      default: return hipErrorInvalidValue;
+    }
   }
   // the follow-up lists are short (the ball list ~0.1 % of the queries, the exact list usually
   // empty): one launch of 64-thread blocks, grid-stride over them; LDS for the group stacks and

@@ -229,7 +229,7 @@ __device__ void finalize_cov_publish(IterDev* it, const CovMoments& g, IterPubli
     rec->pad[0] = (double)(pub.lists[0] + pub.lists[3]);
     rec->pad[1] = (double)pub.lists[1];
     rec->pad[2] = (double)pub.lists[2];
-    for (int k = 0; k < 4; k++) pub.lists[k] = 0u;
+    for (int k = 0; k < 5; k++) pub.lists[k] = 0u;  // + the half list of the wave search
     it->c_global = rec->c_global;
     it->rmse = rec->rmse;
   }

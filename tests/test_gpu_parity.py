@@ -426,3 +426,22 @@ def test_session_step_n_equals_steps(icp):
     nb, Tb = run(False)
     assert na == nb and 0 < na <= 40
     assert np.array_equal(Ta, Tb)
+
+
+def test_overflowing_waves_take_the_half_pass(icp, oracle):
+    """A wave whose search box overflows its candidate list (the first iterate's descent guesses,
+    at 1M: ~16 % of the waves) is searched again as two 32-query halves with their own smaller
+    boxes (k_nn_half) before anything goes to the ball search; every result stays the reference's."""
+    tgt, src, _ = icp.synth_pair(1_000_000)
+    with icp.Context(0, {"debug_counters": 1}) as ctx:
+        ctx.set_target(tgt, 10, 20, icp.RULES_ENGINE)
+        ctx.set_source(src)
+        st = ctx.iterate(None, 0, icp.RULES_ENGINE, 3.0)
+        c = ctx.debug_counters()
+        idx, d = ctx.get_correspondences()
+    assert c["overflow_waves"] > 0 and c["halves"] > 0, c
+    oidx, od = oracle.OracleTree(tgt).nn(src, init_best=oracle.DBL_MAX)
+    np.testing.assert_array_equal(idx, oidx)
+    np.testing.assert_array_equal(d, od)
+    # the halves took most of the overflowed queries off the ball search
+    assert st.n_ball_search < 64 * c["overflow_waves"], (st.n_ball_search, c)
