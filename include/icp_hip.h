@@ -90,9 +90,10 @@ typedef struct icp_hip_config {
                              and 1/2 cost +4 % search time          dflt 0 */
   int32_t query_order;    /* the kd order of the source queries (64-query buckets = waves):
                              0: built on the device; 1: on the host (query_order.cpp)  dflt 0 */
-  int32_t overflow_halves; /* 1: the queries of a wave whose search box overflows are searched
-                              again as two 32-query halves (k_nn_half) before the ball search;
-                              0: they go to the ball search                             dflt 1 */
+  int32_t overflow_halves; /* 1: in the first iterate of a source (descent guesses, ~16 % of
+                              the waves overflow), the queries of a wave whose search box
+                              overflows are searched again as two 32-query halves (k_nn_half)
+                              before the ball search; 0: they go to the ball search     dflt 1 */
   int32_t reserved[4];    /* zero */
 } icp_hip_config;
 

@@ -547,7 +547,10 @@ int icp_hip_iterate(icp_hip_ctx* c, const double* T_apply, int iter, int rules, 
     for (int k = 0; k < 12; k++) a.T[k] = T_apply[k];
   a.fb_list = c->fb_list;
   a.fb_list2 = c->fb_list + c->n_src;
-  a.fb_list3 = c->cfg.overflow_halves ? c->fb_list + 2 * c->n_src : nullptr;  // 2 (n/32 + 2) <= n + 64 ints
+  // the half pass pays off where many waves overflow: the first iterate of a source (descent
+  // guesses, loose boxes; ~16 % of the waves at 10M). Later iterates overflow in ~0.2 % of the
+  // waves, whose queries the ball search finishes sooner than a second serial launch.
+  a.fb_list3 = (c->cfg.overflow_halves && !c->have_prev) ? c->fb_list + 2 * c->n_src : nullptr;  // <= n + 64 ints
   a.fb_u2 = c->fb_u;
   a.fb_count = c->fb_count;
   a.have_prev = c->have_prev ? 1 : 0;

@@ -73,21 +73,56 @@ __device__ CovSums covsum_merge(const CovSums& a, const CovSums& b) {
   return r;
 }
 
-// The shifts of this iteration: query 0's residual, its source point and its match (a function of
-// this iteration's data only, so equal inputs give equal bits; every block and the last level
-// compute the same values). Any finite shift is correct; one inside the data keeps the sums at
-// the scale of the data's spread.
-__device__ __forceinline__ double moment_shift(const double* dist, int64_t n) {
-  const double d0 = n > 0 ? dist[0] : 0.0;
-  return __builtin_isfinite(d0) ? d0 : 0.0;
+// The shifts of this iteration, from the first 64 queries (a function of this iteration's data
+// only, so equal inputs give equal bits; every block and the last level compute the same values).
+// Any finite shift is correct; one inside the bulk of the data keeps the sums at the scale of the
+// data's spread instead of its offset (LAS-sized coordinates) or an outlier's (a far query whose
+// residual is 1e10 would otherwise cancel every other pair's digits):
+//   residuals: the smallest finite residual of the first 64 (outliers are large residuals);
+//   pairs: the first VALID pair (d <= threshold) of the first 64, else query 0's.
+// Computed by the block's first wave; `sm` (>= 6 doubles of LDS) carries them to the block.
+__device__ double moment_shift_block(const double* dist, int64_t n, double* sm) {
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    const double d = lane < n ? dist[lane] : __builtin_inf();
+    const double m = wave_min_d(__builtin_isfinite(d) ? d : __builtin_inf());
+    if (lane == 0) sm[0] = __builtin_isfinite(m) ? m : 0.0;
+  }
+  __syncthreads();
+  const double c = sm[0];
+  __syncthreads();
+  return c;
 }
-__device__ __forceinline__ void cov_shift(const double* x, const double* y, const double* z, const int32_t* pos,
-                                          const TgtPt* pts, int64_t n, double sh[6]) {
-  for (int k = 0; k < 6; k++) sh[k] = 0.0;
-  if (n <= 0) return;
-  const TgtPt p = pts[pos[0]];
-  const double v[6] = {x[0], y[0], z[0], p.x, p.y, p.z};
-  for (int k = 0; k < 6; k++) sh[k] = __builtin_isfinite(v[k]) ? v[k] : 0.0;
+
+__device__ void cov_shift_block(const double* x, const double* y, const double* z, const int32_t* pos,
+                                const TgtPt* pts, int64_t n, double thr, double sh[6], double* sm) {
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    double v[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    bool valid = false;
+    if (lane < n) {
+      const TgtPt p = pts[pos[lane]];
+      v[0] = x[lane];
+      v[1] = y[lane];
+      v[2] = z[lane];
+      v[3] = p.x;
+      v[4] = p.y;
+      v[5] = p.z;
+      const double ex = v[3] - v[0], ey = v[4] - v[1], ez = v[5] - v[2];
+      valid = __builtin_sqrt(ex * ex + ey * ey + ez * ez) <= thr;
+    }
+    const unsigned long long vm = __ballot(valid);
+    const int src = vm ? __builtin_ctzll(vm) : 0;
+#pragma unroll
+    for (int k = 0; k < 6; k++) {
+      const double w = readlane_d(v[k], src);
+      if (lane == 0) sm[k] = __builtin_isfinite(w) ? w : 0.0;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 6; k++) sh[k] = sm[k];
+  __syncthreads();
 }
 
 // Residual moments of the rank's queries in fixed parts of kMomPart queries, once every search
@@ -98,7 +133,7 @@ constexpr int kMomPart = 256 * kMomPer;
 
 __global__ void __launch_bounds__(256) k_moments(const double* __restrict__ dist, int64_t n, MomSums* part) {
   __shared__ double red[4 * 4];
-  const double c = moment_shift(dist, n);
+  const double c = moment_shift_block(dist, n, red);
   const int64_t b0 = (int64_t)blockIdx.x * kMomPart + threadIdx.x;
   double v[4] = {0.0, 0.0, 0.0, 0.0};  // count, sum (d - c), sum (d - c)^2, non-finite
   double mn = 1.7976931348623157e308, mx = 0.0;
@@ -184,9 +219,10 @@ __device__ void finalize_moments(IterDev* it, const Moments& g, const MomentsFin
 __global__ void __launch_bounds__(256) k_merge_moments_last(const MomSums* in, int64_t n, const double* dist,
                                                            int64_t nq, IterDev* it, MomentsFinalize fin, int finalize) {
   __shared__ MomSums sm[256];
+  __shared__ double shs[1];
+  const double c = moment_shift_block(dist, nq, shs);
   const MomSums r = block_tree_last<MomSums, momsum_merge, momsum_identity>(in, n, sm);
   if (threadIdx.x == 0) {
-    const double c = moment_shift(dist, nq);
     Moments m = moments_identity();
     if (r.n > 0.0) {
       m.n = r.n;
@@ -246,11 +282,12 @@ __global__ void __launch_bounds__(256) k_merge_cov_last(const CovSums* in, int64
                                                        IterPublish pub, int finalize) {
   __shared__ CovSums sm[256];
   __shared__ IterDev rec;
+  __shared__ double shs[6];
+  double sh[6];
+  cov_shift_block(cl.x, cl.y, cl.z, cl.pos, cl.pts, cl.n, cl.it->thr, sh, shs);
   const CovSums r = block_tree_last<CovSums, covsum_merge, covsum_identity>(in, n, sm);
   __shared__ CovMoments res;
   if (threadIdx.x == 0) {
-    double sh[6];
-    cov_shift(cl.x, cl.y, cl.z, cl.pos, cl.pts, cl.n, sh);
     CovMoments m = cov_identity();
     if (r.n > 0.0) {
       m.n = r.n;
@@ -293,7 +330,7 @@ __global__ void __launch_bounds__(256) k_cull_cov(CullLaunch a) {
   __shared__ double red[4 * 17];
   const double thr = a.it->thr;
   double sh[6];
-  cov_shift(a.x, a.y, a.z, a.pos, a.pts, a.n, sh);
+  cov_shift_block(a.x, a.y, a.z, a.pos, a.pts, a.n, thr, sh, red);
   const int64_t base = (int64_t)blockIdx.x * (256 * kCullPer) + threadIdx.x;
   // count, sum d^2, sum (a - s), sum (b - t), sum (a - s)(b - t)^T over the valid pairs
   double v[17];

@@ -263,7 +263,7 @@ def test_fallback_share_small_on_scans(icp, gpu_ctx):
                                    (300_000, {"xcd_blocks": 0}),
                                    (1_000_000, {"candidate_cache": 0}), (300_000, {"candidate_margin": 0}),
                                    (300_000, {"candidate_margin": 256}),
-                                   (1_000_000, {"query_order": 1}), (1_000_000, {"certify_prev": 3}),
+                                   (1_000_000, {"overflow_halves": 0}), (1_000_000, {"certify_prev": 3}),
                                    (300_000, {"certify_prev": 2, "candidate_cache": 0})])
 def test_scan32_matches_fp64_scan(icp, n, cfg):
     """Every configuration of the certified search (fp32 filter scan vs fp64 scan, cell-table
@@ -445,3 +445,56 @@ def test_overflowing_waves_take_the_half_pass(icp, oracle):
     np.testing.assert_array_equal(d, od)
     # the halves took most of the overflowed queries off the ball search
     assert st.n_ball_search < 64 * c["overflow_waves"], (st.n_ball_search, c)
+
+
+def test_host_and_device_query_orders(icp, oracle):
+    """The source's kd order built on the device (default) or on the host (query_order = 1): the
+    first iterate searches the same queries, so identical correspondences and residuals; later
+    iterates move the queries by transforms whose statistics were summed in another query order
+    (rounding only): transforms within 1e-12, correspondences equal."""
+    tgt, src, _ = icp.synth_pair(1_000_000)
+
+    def run(conf):
+        out = []
+        with icp.Context(0, conf) as ctx:
+            ctx.set_target(tgt, 10, 20, icp.RULES_ENGINE)
+            ctx.set_source(src)
+            sess = ctx.session(icp.params_default(max_iterations=4, tolerance=0.0))
+            for _ in range(4):
+                rec = sess.step()
+                out.append(ctx.get_correspondences() + (np.array(rec.transform[:]),))
+            sess.close()
+        return out
+
+    dev, host = run({"query_order": 0}), run({"query_order": 1})
+    np.testing.assert_array_equal(dev[0][0], host[0][0])
+    np.testing.assert_array_equal(dev[0][1], host[0][1])
+    for (ia, da, Ta), (ib, db, Tb) in zip(dev, host):
+        np.testing.assert_array_equal(ia, ib)
+        np.testing.assert_allclose(da, db, rtol=1e-10)
+        np.testing.assert_allclose(Ta, Tb, rtol=0, atol=1e-12)
+    oidx, od = oracle.OracleTree(tgt).nn(src, init_best=oracle.DBL_MAX)
+    np.testing.assert_array_equal(dev[0][0], oidx)
+    np.testing.assert_array_equal(dev[0][1], od)
+
+
+def test_outlier_first_query_keeps_statistics_precise(icp, oracle):
+    """Far outliers (3e10 m) wherever the query order puts them, the first slot included: the
+    shifts of the moment and covariance sums come from the bulk of the data (the smallest finite
+    residual / the first valid pair of the first 64 queries), not from an outlier, so the
+    transform matches the oracle's to 1e-10 (an outlier shift cancelled ~6 digits)."""
+    rng = np.random.default_rng(17)
+    t = rng.normal(size=(3000, 3)) * [4, 4, 1]
+    far = np.array([[-3e10, -3e10, -3e10], [3e10, -2e10, 1e10], [-1e10, 3e10, -2e10], [2e10, 1e10, 3e10]])
+    s = np.concatenate([far, t[:1500] + rng.normal(size=(1500, 3)) * 0.01 + [0.05, -0.02, 0.01]])
+    p = icp.params_default(max_iterations=6, tolerance=0.0)
+    for conf in ({"query_order": 0}, {"query_order": 1}):
+        with icp.Context(0, conf) as ctx:
+            ctx.set_target(t, 10, 20, icp.RULES_ENGINE)
+            ctx.set_source(s)
+            rc, res, hist = ctx.run(p)
+        orc, ores, ohist, _ = oracle.icp(s, t, oracle.SEM_ENGINE, 6, 0.0)
+        oh = [h for h in ohist if h.has_transform]
+        assert [h.valid_points for h in hist] == [h.valid for h in oh]
+        for h, o in zip(hist, oh):
+            np.testing.assert_allclose(np.array(h.transform), np.array(o.T_cum), rtol=0, atol=1e-10)
