@@ -568,14 +568,6 @@ int icp_hip_iterate(icp_hip_ctx* c, const double* T_apply, int iter, int rules, 
   // residual moments -> mean, std, threshold (no communicator: fused into the last merge level)
   const bool multi = c->comm != nullptr || c->xfn != nullptr;
   const MomentsFinalize fin{sigma_multiplier, iter, rules == ICP_RULES_ENGINE ? 1 : 0};
-  HIP_TRY(launch_moments(c->dist, c->n_src, c->mparts, s));
-  HIP_TRY(launch_merge_moments(c->mparts, c->nb_mom, c->dist, c->n_src, c->it, multi ? nullptr : &fin, s));
-  if (multi) {
-    const int rc = all_gather_record(c, reinterpret_cast<const double*>(&c->it->m_local),
-                                     reinterpret_cast<double*>(c->gm), (int)(sizeof(Moments) / sizeof(double)), s);
-    if (rc != ICP_HIP_OK) return rc;
-    HIP_TRY(launch_finalize_moments(c->gm, c->nranks, c->it, fin, s));
-  }
   CullLaunch cl;
   cl.x = c->x;
   cl.y = c->y;
@@ -585,6 +577,14 @@ int icp_hip_iterate(icp_hip_ctx* c, const double* T_apply, int iter, int rules, 
   cl.it = c->it;
   cl.part = c->cparts;
   cl.n = c->n_src;
+  HIP_TRY(launch_moments(c->dist, c->n_src, c->mparts, s));
+  HIP_TRY(launch_merge_moments(c->mparts, c->nb_mom, c->dist, c->n_src, c->it, multi ? nullptr : &fin, cl, s));
+  if (multi) {
+    const int rc = all_gather_record(c, reinterpret_cast<const double*>(&c->it->m_local),
+                                     reinterpret_cast<double*>(c->gm), (int)(sizeof(Moments) / sizeof(double)), s);
+    if (rc != ICP_HIP_OK) return rc;
+    HIP_TRY(launch_finalize_moments(c->gm, c->nranks, c->it, fin, cl, s));
+  }
   HIP_TRY(launch_cull_cov(cl, s));
   // covariance moments -> RMSE; the finished record is stored into pinned host memory
   const uint64_t seq = ++c->publish_seq;

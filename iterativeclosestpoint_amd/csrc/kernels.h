@@ -20,6 +20,7 @@ struct IterDev {
   CovMoments c_local;   // this rank's valid-pair moments
   CovMoments c_global;  // merged over ranks
   double mean, sd, thr, rmse;
+  double cshift[6];  // this iteration's shift of the pair sums (set with the threshold)
   double pad[4];
 };
 
@@ -86,6 +87,17 @@ hipError_t launch_nn(const NNLaunch& a, hipStream_t s);
 // TgtPt::sep of every target point (lower bound of its distance to every other point).
 hipError_t launch_target_sep(const NodeRec* nodes, TgtPt* pts, int64_t n, int levels, hipStream_t s);
 
+struct CullLaunch {
+  const double* x;
+  const double* y;
+  const double* z;
+  const int32_t* pos;
+  const TgtPt* pts;
+  const IterDev* it;
+  CovMoments* part;
+  int64_t n;
+};
+
 // Residual moments of the settled queries in fixed parts (deterministic), then the merges.
 int64_t moments_num_parts(int64_t n);
 hipError_t launch_moments(const double* dist, int64_t n, Moments* part, hipStream_t s);
@@ -97,12 +109,13 @@ struct MomentsFinalize {
   int iter;
   int engine_rules;
 };
-// Merge the rank's partials into it->m_local; with fin (no communicator) also mean/std/threshold.
+// Merge the rank's partials into it->m_local; with fin (no communicator) also mean/std/threshold
+// and the cull's pair shift (it->cshift, from cl's first 64 queries).
 hipError_t launch_merge_moments(const Moments* part, int64_t nparts, const double* dist, int64_t nq, IterDev* it,
-                                const MomentsFinalize* fin, hipStream_t s);
+                                const MomentsFinalize* fin, const CullLaunch& cl, hipStream_t s);
 // Merge `nranks` gathered moments in rank order and compute mean/std/threshold.
 hipError_t launch_finalize_moments(const Moments* gathered, int nranks, IterDev* it, MomentsFinalize fin,
-                                   hipStream_t s);
+                                   const CullLaunch& cl, hipStream_t s);
 
 // Where the finished record goes: a device-visible pinned host IterDev (list sizes in pad[0..2]);
 // the three list counters are reset for the next search.
@@ -112,16 +125,7 @@ struct IterPublish {
   double seq;  // stored last into host->pad[3]: the record is complete
 };
 
-struct CullLaunch {
-  const double* x;
-  const double* y;
-  const double* z;
-  const int32_t* pos;
-  const TgtPt* pts;
-  const IterDev* it;
-  CovMoments* part;
-  int64_t n;
-};
+
 int64_t cull_num_blocks(int64_t n);
 hipError_t launch_cull_cov(const CullLaunch& a, hipStream_t s);
 // Merge the rank's partials into it->c_local; with pub (no communicator) also RMSE + publish.

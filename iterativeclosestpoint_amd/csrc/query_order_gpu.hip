@@ -34,30 +34,10 @@ __device__ __forceinline__ uint32_t okey(float f) {  // order-preserving (non-Na
   return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
 }
 
-// One workgroup per segment: the longest axis of its bounding box (ties: the lower axis, as the
-// host's strict > scan).
-__global__ void __launch_bounds__(256) k_seg_axis(const double* __restrict__ xyz, const int32_t* __restrict__ perm,
-                                                  const int32_t* __restrict__ starts,
-                                                  const int32_t* __restrict__ sizes, int bucket,
-                                                  uint8_t* __restrict__ axis) {
-  __shared__ float red[6][4];
-  const int seg = blockIdx.x;
-  const int32_t s0 = starts[seg], sz = sizes[seg];
-  if (sz <= bucket) {  // finished: never split again
-    if (threadIdx.x == 0) axis[seg] = 0;
-    return;
-  }
-  float lo[3] = {__builtin_inff(), __builtin_inff(), __builtin_inff()};
-  float hi[3] = {-__builtin_inff(), -__builtin_inff(), -__builtin_inff()};
-  for (int32_t k = threadIdx.x; k < sz; k += blockDim.x) {
-    const int64_t j = perm[s0 + k];
-#pragma unroll
-    for (int a = 0; a < 3; a++) {
-      const float v = coord32(xyz[3 * j + a]);
-      lo[a] = v < lo[a] ? v : lo[a];
-      hi[a] = v > hi[a] ? v : hi[a];
-    }
-  }
+constexpr int32_t kChunk = 16384;  // segments larger than this take their box from chunks
+
+// block-wide min/max of 3 lo + 3 hi floats into red[6][blockDim/64]; thread 0 gets the results
+__device__ __forceinline__ void block_box(float lo[3], float hi[3], float (*red)[4]) {
 #pragma unroll
   for (int a = 0; a < 3; a++) {
     for (int o = 32; o >= 1; o >>= 1) {
@@ -75,20 +55,93 @@ __global__ void __launch_bounds__(256) k_seg_axis(const double* __restrict__ xyz
   __syncthreads();
   if (threadIdx.x == 0) {
     const int nw = blockDim.x >> 6;
-    float e[3];
     for (int a = 0; a < 3; a++) {
       float l = red[a][0], h = red[3 + a][0];
       for (int q = 1; q < nw; q++) {
         l = red[a][q] < l ? red[a][q] : l;
         h = red[3 + a][q] > h ? red[3 + a][q] : h;
       }
-      e[a] = h - l;
+      lo[a] = l;
+      hi[a] = h;
     }
-    int ax = 0;
-    for (int a = 1; a < 3; a++)
-      if (e[a] > e[ax]) ax = a;
-    axis[seg] = (uint8_t)ax;
   }
+}
+
+__device__ __forceinline__ uint8_t longest_axis(const float lo[3], const float hi[3]) {
+  int ax = 0;
+  for (int a = 1; a < 3; a++)
+    if (hi[a] - lo[a] > hi[ax] - lo[ax]) ax = a;
+  return (uint8_t)ax;
+}
+
+// Big segments: the box of each chunk of kChunk slots (one workgroup each) ...
+__global__ void __launch_bounds__(256) k_chunk_bbox(const double* __restrict__ xyz, const int32_t* __restrict__ perm,
+                                                    const int32_t* __restrict__ cstart, const int32_t* __restrict__ clen,
+                                                    float* __restrict__ cbox) {
+  __shared__ float red[6][4];
+  const int c = blockIdx.x;
+  const int32_t s0 = cstart[c], n = clen[c];
+  float lo[3] = {__builtin_inff(), __builtin_inff(), __builtin_inff()};
+  float hi[3] = {-__builtin_inff(), -__builtin_inff(), -__builtin_inff()};
+  for (int32_t k = threadIdx.x; k < n; k += blockDim.x) {
+    const int64_t j = perm[s0 + k];
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+      const float v = coord32(xyz[3 * j + a]);
+      lo[a] = v < lo[a] ? v : lo[a];
+      hi[a] = v > hi[a] ? v : hi[a];
+    }
+  }
+  block_box(lo, hi, red);
+  if (threadIdx.x == 0)
+    for (int a = 0; a < 3; a++) {
+      cbox[6 * c + a] = lo[a];
+      cbox[6 * c + 3 + a] = hi[a];
+    }
+}
+
+// ... then each big segment's axis from its chunks' boxes (one thread per big segment).
+__global__ void k_big_axis(const float* __restrict__ cbox, const int32_t* __restrict__ bseg,
+                           const int32_t* __restrict__ bfirst, int nbig, uint8_t* __restrict__ axis) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= nbig) return;
+  float lo[3] = {__builtin_inff(), __builtin_inff(), __builtin_inff()};
+  float hi[3] = {-__builtin_inff(), -__builtin_inff(), -__builtin_inff()};
+  for (int c = bfirst[b]; c < bfirst[b + 1]; c++)
+    for (int a = 0; a < 3; a++) {
+      lo[a] = cbox[6 * c + a] < lo[a] ? cbox[6 * c + a] : lo[a];
+      hi[a] = cbox[6 * c + 3 + a] > hi[a] ? cbox[6 * c + 3 + a] : hi[a];
+    }
+  axis[bseg[b]] = longest_axis(lo, hi);
+}
+
+// One workgroup per segment: the longest axis of its bounding box (ties: the lower axis, as the
+// host's strict > scan).
+__global__ void __launch_bounds__(256) k_seg_axis(const double* __restrict__ xyz, const int32_t* __restrict__ perm,
+                                                  const int32_t* __restrict__ starts,
+                                                  const int32_t* __restrict__ sizes, int bucket,
+                                                  uint8_t* __restrict__ axis) {
+  __shared__ float red[6][4];
+  const int seg = blockIdx.x;
+  const int32_t s0 = starts[seg], sz = sizes[seg];
+  if (sz > kChunk) return;  // a big segment: the chunk path (k_chunk_bbox, k_big_axis)
+  if (sz <= bucket) {  // finished: never split again
+    if (threadIdx.x == 0) axis[seg] = 0;
+    return;
+  }
+  float lo[3] = {__builtin_inff(), __builtin_inff(), __builtin_inff()};
+  float hi[3] = {-__builtin_inff(), -__builtin_inff(), -__builtin_inff()};
+  for (int32_t k = threadIdx.x; k < sz; k += blockDim.x) {
+    const int64_t j = perm[s0 + k];
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+      const float v = coord32(xyz[3 * j + a]);
+      lo[a] = v < lo[a] ? v : lo[a];
+      hi[a] = v > hi[a] ? v : hi[a];
+    }
+  }
+  block_box(lo, hi, red);
+  if (threadIdx.x == 0) axis[seg] = longest_axis(lo, hi);
 }
 
 // Sort key of every slot: its segment's start (high word) and its coordinate on that segment's axis.
@@ -174,6 +227,8 @@ hipError_t gpu_kd_query_order(const double* d_xyz, int64_t n, int bucket, int32_
   int32_t *d_starts = nullptr, *d_sizes = nullptr, *perm_alt = nullptr;
   uint8_t* d_axis = nullptr;
   uint64_t *keys = nullptr, *keys_alt = nullptr;
+  void* d_chunks = nullptr;  // chunk boxes + chunk / big-segment tables
+  size_t chunk_cap = 0;
   void* tmp = nullptr;
   size_t tmp_bytes = 0;
   int sbits = 1;
@@ -192,6 +247,41 @@ hipError_t gpu_kd_query_order(const double* d_xyz, int64_t n, int bucket, int32_
     const int nseg = (int)lv_start[L].size();
     QO_TRY(hipMemcpyAsync(d_starts, lv_start[L].data(), nseg * sizeof(int32_t), hipMemcpyHostToDevice, s));
     QO_TRY(hipMemcpyAsync(d_sizes, lv_size[L].data(), nseg * sizeof(int32_t), hipMemcpyHostToDevice, s));
+    {
+      // big segments (the top levels): their boxes from chunks of kChunk slots, many workgroups each
+      std::vector<int32_t> cst, cln, bseg, bfirst{0};
+      for (int k = 0; k < nseg; k++) {
+        if (lv_size[L][k] <= kChunk) continue;
+        for (int32_t o = 0; o < lv_size[L][k]; o += kChunk) {
+          cst.push_back(lv_start[L][k] + o);
+          cln.push_back(std::min(kChunk, lv_size[L][k] - o));
+        }
+        bseg.push_back(k);
+        bfirst.push_back((int32_t)cst.size());
+      }
+      if (!bseg.empty()) {
+        const size_t nc = cst.size(), nb = bseg.size();
+        if (nc > chunk_cap) {
+          if (d_chunks) (void)hipFree(d_chunks);
+          d_chunks = nullptr;
+          chunk_cap = nc;
+          QO_TRY(hipMalloc(reinterpret_cast<void**>(&d_chunks), chunk_cap * (6 * sizeof(float) + 3 * sizeof(int32_t)) +
+                                                                 2 * sizeof(int32_t)));
+        }
+        float* cbox = reinterpret_cast<float*>(d_chunks);
+        int32_t* ci = reinterpret_cast<int32_t*>(cbox + 6 * chunk_cap);
+        QO_TRY(hipMemcpyAsync(ci, cst.data(), nc * sizeof(int32_t), hipMemcpyHostToDevice, s));
+        QO_TRY(hipMemcpyAsync(ci + chunk_cap, cln.data(), nc * sizeof(int32_t), hipMemcpyHostToDevice, s));
+        QO_TRY(hipMemcpyAsync(ci + 2 * chunk_cap, bseg.data(), nb * sizeof(int32_t), hipMemcpyHostToDevice, s));
+        QO_TRY(hipMemcpyAsync(ci + 2 * chunk_cap + nb, bfirst.data(), (nb + 1) * sizeof(int32_t),
+                              hipMemcpyHostToDevice, s));
+        hipLaunchKernelGGL(k_chunk_bbox, dim3((unsigned)nc), dim3(256), 0, s, d_xyz, d_perm, ci, ci + chunk_cap, cbox);
+        hipLaunchKernelGGL(k_big_axis, dim3(grid_for((int64_t)nb, 64)), dim3(64), 0, s, cbox, ci + 2 * chunk_cap,
+                           ci + 2 * chunk_cap + nb, (int)nb, d_axis);
+        QO_TRY(hipGetLastError());
+        QO_TRY(hipStreamSynchronize(s));  // the host tables are read by the copies above
+      }
+    }
     const int32_t big = *std::max_element(lv_size[L].begin(), lv_size[L].end());
     const int bs = big <= 128 ? 64 : 256;  // deep levels: one wave per (small) segment
     hipLaunchKernelGGL(k_seg_axis, dim3((unsigned)nseg), dim3(bs), 0, s, d_xyz, d_perm, d_starts, d_sizes, bucket,
@@ -207,7 +297,8 @@ hipError_t gpu_kd_query_order(const double* d_xyz, int64_t n, int bucket, int32_
   }
 done:
   (void)hipStreamSynchronize(s);
-  for (void* p : {(void*)d_starts, (void*)d_sizes, (void*)d_axis, (void*)perm_alt, (void*)keys, (void*)keys_alt, tmp})
+  for (void* p : {(void*)d_starts, (void*)d_sizes, (void*)d_axis, (void*)perm_alt, (void*)keys, (void*)keys_alt, tmp,
+                  d_chunks})
     if (p) (void)hipFree(p);
   return err;
 }

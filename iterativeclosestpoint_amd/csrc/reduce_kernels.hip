@@ -94,8 +94,10 @@ __device__ double moment_shift_block(const double* dist, int64_t n, double* sm) 
   return c;
 }
 
-__device__ void cov_shift_block(const double* x, const double* y, const double* z, const int32_t* pos,
-                                const TgtPt* pts, int64_t n, double thr, double sh[6], double* sm) {
+// The pair-sum shift, once per iteration by the kernel that sets the threshold (its first wave),
+// into it->cshift: the cull blocks and the last merge level read it from there.
+__device__ void cov_shift_store(const double* x, const double* y, const double* z, const int32_t* pos,
+                                const TgtPt* pts, int64_t n, double thr, IterDev* it) {
   if (threadIdx.x < 64) {
     const int lane = threadIdx.x;
     double v[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
@@ -116,13 +118,9 @@ __device__ void cov_shift_block(const double* x, const double* y, const double* 
 #pragma unroll
     for (int k = 0; k < 6; k++) {
       const double w = readlane_d(v[k], src);
-      if (lane == 0) sm[k] = __builtin_isfinite(w) ? w : 0.0;
+      if (lane == 0) it->cshift[k] = __builtin_isfinite(w) ? w : 0.0;
     }
   }
-  __syncthreads();
-#pragma unroll
-  for (int k = 0; k < 6; k++) sh[k] = sm[k];
-  __syncthreads();
 }
 
 // Residual moments of the rank's queries in fixed parts of kMomPart queries, once every search
@@ -217,11 +215,34 @@ __device__ void finalize_moments(IterDev* it, const Moments& g, const MomentsFin
 // Last level of the rank's moments: the summed part -> (count, mean, M2) in it->m_local; with fin
 // (one rank, no communicator) also the statistics.
 __global__ void __launch_bounds__(256) k_merge_moments_last(const MomSums* in, int64_t n, const double* dist,
-                                                           int64_t nq, IterDev* it, MomentsFinalize fin, int finalize) {
+                                                           int64_t nq, IterDev* it, MomentsFinalize fin, int finalize,
+                                                           CullLaunch cl) {
   __shared__ MomSums sm[256];
   __shared__ double shs[1];
   const double c = moment_shift_block(dist, nq, shs);
   const MomSums r = block_tree_last<MomSums, momsum_merge, momsum_identity>(in, n, sm);
+  if (finalize) {
+    // the threshold, then the pair shift of the cull (its first wave)
+    __shared__ double thr_s;
+    if (threadIdx.x == 0) {
+      Moments m = moments_identity();
+      if (r.n > 0.0) {
+        m.n = r.n;
+        m.mean = c + r.s1 / r.n;
+        const double m2 = r.s2 - r.s1 * (r.s1 / r.n);
+        m.m2 = m2 < 0.0 ? 0.0 : m2;
+        m.dmin = r.dmin;
+        m.dmax = r.dmax;
+      }
+      m.nbad = r.nbad;
+      it->m_local = m;
+      finalize_moments(it, m, fin);
+      thr_s = it->thr;
+    }
+    __syncthreads();
+    cov_shift_store(cl.x, cl.y, cl.z, cl.pos, cl.pts, cl.n, thr_s, it);
+    return;
+  }
   if (threadIdx.x == 0) {
     Moments m = moments_identity();
     if (r.n > 0.0) {
@@ -234,15 +255,20 @@ __global__ void __launch_bounds__(256) k_merge_moments_last(const MomSums* in, i
     }
     m.nbad = r.nbad;
     it->m_local = m;
-    if (finalize) finalize_moments(it, m, fin);
   }
 }
 
-__global__ void k_finalize_moments(const Moments* gathered, int nranks, IterDev* it, MomentsFinalize fin) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  Moments g = gathered[0];
-  for (int r = 1; r < nranks; r++) g = moments_merge(g, gathered[r]);  // rank order: same bits everywhere
-  finalize_moments(it, g, fin);
+__global__ void __launch_bounds__(64) k_finalize_moments(const Moments* gathered, int nranks, IterDev* it,
+                                                         MomentsFinalize fin, CullLaunch cl) {
+  __shared__ double thr_s;
+  if (threadIdx.x == 0) {
+    Moments g = gathered[0];
+    for (int r = 1; r < nranks; r++) g = moments_merge(g, gathered[r]);  // rank order: same bits everywhere
+    finalize_moments(it, g, fin);
+    thr_s = it->thr;
+  }
+  __syncthreads();
+  cov_shift_store(cl.x, cl.y, cl.z, cl.pos, cl.pts, cl.n, thr_s, it);
 }
 
 // The iteration's record goes straight into the caller's pinned host buffer (no copy engine or
@@ -282,9 +308,9 @@ __global__ void __launch_bounds__(256) k_merge_cov_last(const CovSums* in, int64
                                                        IterPublish pub, int finalize) {
   __shared__ CovSums sm[256];
   __shared__ IterDev rec;
-  __shared__ double shs[6];
   double sh[6];
-  cov_shift_block(cl.x, cl.y, cl.z, cl.pos, cl.pts, cl.n, cl.it->thr, sh, shs);
+#pragma unroll
+  for (int k = 0; k < 6; k++) sh[k] = it->cshift[k];
   const CovSums r = block_tree_last<CovSums, covsum_merge, covsum_identity>(in, n, sm);
   __shared__ CovMoments res;
   if (threadIdx.x == 0) {
@@ -330,7 +356,8 @@ __global__ void __launch_bounds__(256) k_cull_cov(CullLaunch a) {
   __shared__ double red[4 * 17];
   const double thr = a.it->thr;
   double sh[6];
-  cov_shift_block(a.x, a.y, a.z, a.pos, a.pts, a.n, thr, sh, red);
+#pragma unroll
+  for (int k = 0; k < 6; k++) sh[k] = a.it->cshift[k];
   const int64_t base = (int64_t)blockIdx.x * (256 * kCullPer) + threadIdx.x;
   // count, sum d^2, sum (a - s), sum (b - t), sum (a - s)(b - t)^T over the valid pairs
   double v[17];
@@ -426,17 +453,17 @@ hipError_t launch_moments(const double* dist, int64_t n, Moments* part, hipStrea
 }
 
 hipError_t launch_merge_moments(const Moments* part, int64_t nparts, const double* dist, int64_t nq, IterDev* it,
-                                const MomentsFinalize* fin, hipStream_t s) {
+                                const MomentsFinalize* fin, const CullLaunch& cl, hipStream_t s) {
   const MomSums* cur = merge_to_last_span<MomSums, momsum_merge, momsum_identity>(
       reinterpret_cast<const MomSums*>(part), &nparts, s);
   hipLaunchKernelGGL(k_merge_moments_last, dim3(1), dim3(256), 0, s, cur, nparts, dist, nq, it,
-                     fin ? *fin : MomentsFinalize{0.0, 0, 0}, fin ? 1 : 0);
+                     fin ? *fin : MomentsFinalize{0.0, 0, 0}, fin ? 1 : 0, cl);
   return hipGetLastError();
 }
 
 hipError_t launch_finalize_moments(const Moments* gathered, int nranks, IterDev* it, MomentsFinalize fin,
-                                   hipStream_t s) {
-  hipLaunchKernelGGL(k_finalize_moments, dim3(1), dim3(64), 0, s, gathered, nranks, it, fin);
+                                   const CullLaunch& cl, hipStream_t s) {
+  hipLaunchKernelGGL(k_finalize_moments, dim3(1), dim3(64), 0, s, gathered, nranks, it, fin, cl);
   return hipGetLastError();
 }
 
