@@ -230,7 +230,9 @@ int icp_hip_copy_target(icp_hip_ctx* ctx, double* box6, int32_t* first, uint32_t
 int icp_hip_target_separation(icp_hip_ctx* ctx, float* sep_out);
 
 /* Upload this rank's source shard (AoS xyz). Queries are reordered on the device along a
- * Morton curve for traversal coherence; every output is returned in the caller's order. */
+ * Morton curve for traversal coherence; every output is returned in the caller's order.
+ * A shard holds fewer than 2^29 points (ICP_HIP_EINVAL otherwise; shard larger clouds over a
+ * device group). */
 int icp_hip_set_source(icp_hip_ctx* ctx, const double* xyz, int64_t n);
 
 /* One ICP iteration body. If T_apply (row-major 4x4) is non-null, src = T_apply * src is applied

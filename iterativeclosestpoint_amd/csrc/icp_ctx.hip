@@ -473,7 +473,9 @@ int icp_hip_target_separation(icp_hip_ctx* c, float* sep_out) {
 int icp_hip_set_source(icp_hip_ctx* c, const double* xyz, int64_t n) {
   if (!c || (!xyz && n > 0) || n < 0) return fail(ICP_HIP_EINVAL, "bad source arguments");
   if (c->group) return group_set_source(c, xyz, n);
-  if (n > (int64_t)0x7fffffff) return fail(ICP_HIP_EINVAL, "source shard larger than INT32_MAX points");
+  // the wave search addresses per-query arrays by 32-bit byte offsets (nn_device.h qat): < 2^29
+  // points per shard (12 GB of coordinates; a larger cloud is sharded over a device group)
+  if (n >= ((int64_t)1 << 29)) return fail(ICP_HIP_EINVAL, "source shard of 2^29 points or more");
   HIP_TRY(hipSetDevice(c->device));
   free_source(c);
   c->n_src = n;

@@ -232,6 +232,14 @@ __device__ __forceinline__ void block_minmax(double& mn, double& mx, double* red
 
 // ---- queries
 
+// Element i of a per-query array addressed by a 32-bit byte offset from the array's (scalar) base:
+// global loads/stores in the saddr + 32-bit voffset form, no 64-bit address per lane (the wave
+// search's 64-bit query index was spilled to scratch). Shards hold < 2^29 queries (set_source).
+template <class T>
+__device__ __forceinline__ T& qat(T* base, int32_t i) {
+  return *reinterpret_cast<T*>(reinterpret_cast<char*>(base) + (uint32_t)i * (uint32_t)sizeof(T));
+}
+
 // Load query i; with APPLY also src = T * src in place, Eigen's order ((T0 x + T1 y) + T2 z) + T3
 // (icpengine.cpp:345; Matrix4d * MatrixXd without FMA on baseline x86-64).
 template <bool APPLY>
@@ -251,6 +259,35 @@ __device__ __forceinline__ void load_query(const NNLaunch& a, int64_t i, bool ac
     qx = nx;
     qy = ny;
     qz = nz;
+  }
+}
+
+// load_query for a 32-bit index (qat addressing; the wave search), WITHOUT the store of the moved
+// query: the wave search stores it with its results (store_query32), so that no store is pending
+// while its first loads are waited for.
+template <bool APPLY>
+__device__ __forceinline__ void load_query32(const NNLaunch& a, int32_t i, bool active, double& qx, double& qy,
+                                             double& qz) {
+  if (!active) return;
+  qx = qat(a.x, i);
+  qy = qat(a.y, i);
+  qz = qat(a.z, i);
+  if (APPLY) {
+    const double nx = ((a.T[0] * qx + a.T[1] * qy) + a.T[2] * qz) + a.T[3];
+    const double ny = ((a.T[4] * qx + a.T[5] * qy) + a.T[6] * qz) + a.T[7];
+    const double nz = ((a.T[8] * qx + a.T[9] * qy) + a.T[10] * qz) + a.T[11];
+    qx = nx;
+    qy = ny;
+    qz = nz;
+  }
+}
+template <bool APPLY>
+__device__ __forceinline__ void store_query32(const NNLaunch& a, int32_t i, bool active, double qx, double qy,
+                                              double qz) {
+  if (APPLY && active) {
+    qat(a.x, i) = qx;
+    qat(a.y, i) = qy;
+    qat(a.z, i) = qz;
   }
 }
 

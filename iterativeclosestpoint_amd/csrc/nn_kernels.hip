@@ -37,6 +37,9 @@
 #ifndef ICP_STAGE_CONTIG
 #define ICP_STAGE_CONTIG 0
 #endif
+#ifndef ICP_SCAN_UNROLL
+#define ICP_SCAN_UNROLL 1
+#endif
 #ifndef ICP_SKIP_PREV_GATHER
 #define ICP_SKIP_PREV_GATHER 0
 #endif
@@ -201,30 +204,35 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
   double4* stage = reinterpret_cast<double4*>(wl);  // after the walk only
   int32_t* plist = queue + kWaveQueue;               // candidate points
 
-  double qx = 0.0, qy = 0.0, qz = 0.0;
-  load_query<APPLY>(a, i, active, qx, qy, qz);
-  const bool finite_q = __builtin_isfinite(qx) && __builtin_isfinite(qy) && __builtin_isfinite(qz);
-  // The wave's cache record (7 words on lanes 0..6) and its first 64 entries, loaded with the
-  // query: a reusing wave has its first chunk before the box is known (unused otherwise).
+  // The first round trip: the query, its previous match (leaf order), the wave's cache record (7
+  // words on lanes 0..6) and its first 64 entries, all issued before any of them is used (a
+  // reusing wave has its first chunk before the box is known; unused otherwise).
   const int32_t i0 = __builtin_amdgcn_readfirstlane(i);
   const uint32_t wid = (uint32_t)i0 >> 6;
   const bool use_wc = !HALF && a.wc_box != nullptr && i0 < a.n;
+  // the previous match, whose fl(d2) is u (read unconditionally: an unused load costs no wait,
+  // while a conditional one is waited for inside its branch)
+  const int32_t prev_pos = qat(a.pos_out, active ? i : 0);
   double hdr = 0.0;
   float4 ent0 = make_float4(0.f, 0.f, 0.f, 0.f);
   if (use_wc) {
     if (lane < 7) hdr = reinterpret_cast<const double*>(a.wc_box + wid)[lane];
     ent0 = a.wc_ents[(size_t)wid * kWaveCandCap + lane];
   }
+  double qx = 0.0, qy = 0.0, qz = 0.0;
+  load_query32<APPLY>(a, i, active, qx, qy, qz);
+  // every load of the first round trip has landed (a real s_waitcnt, which the compiler's wait
+  // bookkeeping sees, on every path: otherwise it waits again inside each branch below)
+  __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
+  const bool finite_q = __builtin_isfinite(qx) && __builtin_isfinite(qy) && __builtin_isfinite(qz);
 
   PCLK(t_p0);
   // Phase 1: the guess (any value is safe: certification also requires best <= u).
   double u = __builtin_inf();
-  int32_t prev_pos = -1;  // the previous match (leaf order), whose fl(d2) is u
-  bool safe = false;      // the previous match certified from its separation: no search
+  bool safe = false;  // the previous match certified from its separation: no search
   if (active && finite_q && a.have_prev) {
     // the previous match is a candidate: its fl(d2) from the moved query bounds the nearest
     // point's (usually well below (previous residual + displacement)^2)
-    prev_pos = a.pos_out[i];
     const TgtPt* pp = a.pts + prev_pos;
     const double2 pxy = *reinterpret_cast<const double2*>(&pp->x);
     const double dx = pxy.x - qx, dy = pxy.y - qy, dz = pp->z - qz;
@@ -287,11 +295,12 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
       }
     }
     if (open == 0 || (a.certify_prev == 3 && __popcll(open) <= kOpenToBall)) {
-      if (safe) a.dist_out[i] = __builtin_sqrt(u);
+      store_query32<APPLY>(a, i, active, qx, qy, qz);
+      if (safe) qat(a.dist_out, i) = __builtin_sqrt(u);
       if (open != 0) {
         if (active && !finite_q) {
-          a.pos_out[i] = a.pos0;
-          a.dist_out[i] = residual_to(a.pts, a.pos0, qx, qy, qz);
+          qat(a.pos_out, i) = a.pos0;
+          qat(a.dist_out, i) = residual_to(a.pts, a.pos0, qx, qy, qz);
         }
         wave_append_u(active && finite_q && !safe, i, u, a.fb_count + 1, a.fb_list2, a.fb_u2);
       }
@@ -724,8 +733,20 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
             atomicAdd(&a.dbg[10], (unsigned long long)mp);
             atomicAdd(&a.dbg[11], 1ull);
           }
+#if ICP_SCAN_UNROLL == 2
+          {
+            int k = 0;
+#pragma unroll 1
+            for (; k + 1 < mp; k += 2) {
+              eval2(st4[kStep * k], st4[kStep * k + 1], 2u * k);
+              eval2(st4[kStep * k + kStep], st4[kStep * k + kStep + 1], 2u * k + 2u);
+            }
+            if (k < mp) eval2(st4[kStep * k], st4[kStep * k + 1], 2u * k);
+          }
+#else
 #pragma unroll 1
           for (int k = 0; k < mp; k++) eval2(st4[kStep * k], st4[kStep * k + 1], 2u * k);
+#endif
           // the winner of this round, if it improved the lane's best: its index from its slot
           if (k1 != k1_in) {
             const uint32_t sl = __float_as_uint(k1) & 63u;
@@ -907,11 +928,12 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
 
   PCLK(t_p4);
   // Phase 5: certify, write, or queue.
+  store_query32<APPLY>(a, i, active, qx, qy, qz);
   bool written = false, to_exact = false, to_lane = false;
   double d = 0.0;
   int32_t pos = bpos;
   if (safe) {
-    a.dist_out[i] = __builtin_sqrt(u);  // settled in phase 1b (the position stays)
+    qat(a.dist_out, i) = __builtin_sqrt(u);  // settled in phase 1b (the position stays)
   } else if (active) {
     if (!finite_q) {
       // NaN: every leaf distance is NaN; inf: the root's distance is inf. Either way the
@@ -929,8 +951,8 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
       to_lane = true;
     }
     if (written) {
-      a.pos_out[i] = pos;
-      a.dist_out[i] = d;
+      qat(a.pos_out, i) = pos;
+      qat(a.dist_out, i) = d;
     }
   }
   wave_append(to_exact, i, a.fb_count, a.fb_list);
