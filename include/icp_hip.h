@@ -94,7 +94,17 @@ typedef struct icp_hip_config {
                               the waves overflow), the queries of a wave whose search box
                               overflows are searched again as two 32-query halves (k_nn_half)
                               before the ball search; 0: they go to the ball search     dflt 1 */
-  int32_t reserved[4];    /* zero */
+  int32_t device_loop;    /* 1: the engine session's batches (icp_session_step_n, icp_engine_run)
+                             run as a device-resident loop: each iteration's last kernel takes
+                             the session's decisions and computes the transform (the host
+                             loop's own code, session_step.h), so the iterations of a batch
+                             run back to back with one host wait per batch (single-device
+                             contexts; multi-device groups and the host exchange step on the
+                             host); 0: the host steps every iteration. The device step (one
+                             lane's fp64 Jacobi SVD, ~8.5 us) costs what the host round trip
+                             does (7-11 us): equal at 10M and 1.25M shards, 5 % slower at 100k
+                                                                            dflt 0 */
+  int32_t reserved[3];    /* zero */
 } icp_hip_config;
 
 /* Slots of icp_hip_debug_counters (summed over the last iterate's search launches). */

@@ -145,6 +145,7 @@ void icp_hip_config_default(icp_hip_config* cfg) {
   cfg->candidate_cache = 1;
   cfg->candidate_margin = 16;
   cfg->overflow_halves = 1;
+  cfg->device_loop = 0;
 }
 
 int icp_hip_create(icp_hip_ctx** out, int device) { return icp_hip_create_ex(out, device, nullptr); }
@@ -168,6 +169,7 @@ int icp_hip_create_ex(icp_hip_ctx** out, int device, const icp_hip_config* cfg) 
   if (conf.overflow_halves != 0 && conf.overflow_halves != 1) return fail(ICP_HIP_EINVAL, "config: overflow_halves must be 0 or 1");
   if (conf.query_order != 0 && conf.query_order != 1) return fail(ICP_HIP_EINVAL, "config: query_order must be 0 or 1");
   if (conf.certify_prev < 0 || conf.certify_prev > 3) return fail(ICP_HIP_EINVAL, "config: certify_prev out of [0, 3]");
+  if (conf.device_loop != 0 && conf.device_loop != 1) return fail(ICP_HIP_EINVAL, "config: device_loop must be 0 or 1");
   if (!(conf.join_factor >= 1.0 && conf.join_factor <= 1e6))
     return fail(ICP_HIP_EINVAL, "config: join_factor out of [1, 1e6]");
   int ndev = 0;
@@ -185,6 +187,7 @@ int icp_hip_create_ex(icp_hip_ctx** out, int device, const icp_hip_config* cfg) 
     return fail(ICP_HIP_EDEVICE, "hipStreamCreate failed");
   }
   for (hipEvent_t* ev : {&c->ev_it0, &c->ev_it1}) (void)hipEventCreate(ev);
+  (void)hipEventCreateWithFlags(&c->ev_batch, hipEventDisableSystemFence);
   // The per-iterate timing ring only measures elapsed times: no system-scope fence on record
   // (a default event's release writes back L2, ~5 us of GPU idle per record between kernels).
   for (auto& r : c->ring)
@@ -193,7 +196,11 @@ int icp_hip_create_ex(icp_hip_ctx** out, int device, const icp_hip_config* cfg) 
       hipHostMalloc(reinterpret_cast<void**>(&c->h_it), sizeof(IterDev), hipHostMallocMapped | hipHostMallocCoherent) !=
           hipSuccess ||
       hipHostGetDevicePointer(reinterpret_cast<void**>(&c->h_it_dev), c->h_it, 0) != hipSuccess ||
-      dalloc(&c->counters, 2) != hipSuccess || dalloc(&c->fb_count, 8) != hipSuccess ||
+      dalloc(&c->counters, 2) != hipSuccess || dalloc(&c->fb_count, 8) != hipSuccess || dalloc(&c->loopd, 1) != hipSuccess ||
+      hipHostMalloc(reinterpret_cast<void**>(&c->h_loop), sizeof(LoopDev)) != hipSuccess ||
+      hipHostMalloc(reinterpret_cast<void**>(&c->h_ring), icp_hip_ctx::kLoopRing * sizeof(LoopRec),
+                    hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+      hipHostGetDevicePointer(reinterpret_cast<void**>(&c->h_ring_dev), c->h_ring, 0) != hipSuccess ||
       (conf.debug_counters && dalloc(&c->dbg, ICP_DBG_SLOTS) != hipSuccess)) {
     icp_hip_destroy(c);
     return fail(ICP_HIP_ENOMEM, "context allocation failed");
@@ -225,6 +232,10 @@ void icp_hip_destroy(icp_hip_ctx* c) {
   dfree(c->gm);
   dfree(c->gc);
   if (c->h_it) (void)hipHostFree(c->h_it);
+  dfree(c->loopd);
+  if (c->h_loop) (void)hipHostFree(c->h_loop);
+  if (c->h_ring) (void)hipHostFree(c->h_ring);
+  if (c->ev_batch) (void)hipEventDestroy(c->ev_batch);
   if (c->comm) (void)ncclCommDestroy(c->comm);
   for (hipEvent_t ev : {c->ev_it0, c->ev_it1})
     if (ev) (void)hipEventDestroy(ev);
@@ -528,23 +539,27 @@ int icp_hip_set_source(icp_hip_ctx* c, const double* xyz, int64_t n) {
   return ICP_HIP_OK;
 }
 
-int icp_hip_iterate(icp_hip_ctx* c, const double* T_apply, int iter, int rules, double sigma_multiplier,
-                    icp_iter_stats* out) {
-  if (!c || !out) return fail(ICP_HIP_EINVAL, "null argument");
-  if (c->group) return group_iterate(c, T_apply, iter, rules, sigma_multiplier, out);
-  if (!c->nodes) return fail(ICP_HIP_ENOTREADY, "target not set");
-  if (!c->x && c->n_src > 0) return fail(ICP_HIP_ENOTREADY, "source not set");
-  HIP_TRY(hipSetDevice(c->device));
+}  // extern "C"
+
+// One iterate enqueued on the context's stream, no wait. Host-driven (loop_slot < 0): the
+// transform T_apply (null: none) is a kernel argument and the last kernel publishes the record
+// with sequence number *seq for the host's poll. Device loop (loop_slot >= 0): the transform is
+// the device session's pending increment (applied when `apply`), the last kernel steps the session
+// and stores the iteration's LoopRec into ring slot loop_slot.
+static int enqueue_iterate(icp_hip_ctx* c, const double* T_apply, bool apply, int iter, int rules,
+                           double sigma_multiplier, int loop_slot, uint64_t* seq_out) {
   hipStream_t s = c->stream;
   hipEvent_t* ev = c->ring[c->n_iterates % icp_hip_ctx::kTimingRing];
+  LoopDev* loop = loop_slot >= 0 ? c->loopd : nullptr;
   NNLaunch a = base_launch(c);
+  a.loop = loop;
   a.x = c->x;
   a.y = c->y;
   a.z = c->z;
   a.pos_out = c->pos;
   a.dist_out = c->dist;
   a.n = c->n_src;
-  a.apply = T_apply ? 1 : 0;
+  a.apply = apply ? 1 : 0;
   if (T_apply)
     for (int k = 0; k < 12; k++) a.T[k] = T_apply[k];
   a.fb_list = c->fb_list;
@@ -571,6 +586,7 @@ int icp_hip_iterate(icp_hip_ctx* c, const double* T_apply, int iter, int rules, 
   const bool multi = c->comm != nullptr || c->xfn != nullptr;
   const MomentsFinalize fin{sigma_multiplier, iter, rules == ICP_RULES_ENGINE ? 1 : 0};
   CullLaunch cl;
+  cl.loop = loop;
   cl.x = c->x;
   cl.y = c->y;
   cl.z = c->z;
@@ -579,7 +595,7 @@ int icp_hip_iterate(icp_hip_ctx* c, const double* T_apply, int iter, int rules, 
   cl.it = c->it;
   cl.part = c->cparts;
   cl.n = c->n_src;
-  HIP_TRY(launch_moments(c->dist, c->n_src, c->mparts, s));
+  HIP_TRY(launch_moments(c->dist, c->n_src, c->mparts, loop, s));
   HIP_TRY(launch_merge_moments(c->mparts, c->nb_mom, c->dist, c->n_src, c->it, multi ? nullptr : &fin, cl, s));
   if (multi) {
     const int rc = all_gather_record(c, reinterpret_cast<const double*>(&c->it->m_local),
@@ -588,9 +604,18 @@ int icp_hip_iterate(icp_hip_ctx* c, const double* T_apply, int iter, int rules, 
     HIP_TRY(launch_finalize_moments(c->gm, c->nranks, c->it, fin, cl, s));
   }
   HIP_TRY(launch_cull_cov(cl, s));
-  // covariance moments -> RMSE; the finished record is stored into pinned host memory
-  const uint64_t seq = ++c->publish_seq;
-  const IterPublish pub{c->h_it_dev, c->fb_count, (double)seq};
+  // covariance moments -> RMSE; the finished record is stored into pinned host memory (host
+  // loop) or steps the device session (device loop)
+  uint64_t seq = 0;
+  IterPublish pub{nullptr, c->fb_count, 0.0, nullptr, nullptr};
+  if (loop) {
+    pub.loop = loop;
+    pub.rec = c->h_ring_dev + loop_slot;
+  } else {
+    seq = ++c->publish_seq;
+    pub.host = c->h_it_dev;
+    pub.seq = (double)seq;
+  }
   HIP_TRY(launch_merge_cov(c->cparts, c->nb_cull, cl, c->it, multi ? nullptr : &pub, s));
   if (multi) {
     const int rc = all_gather_record(c, reinterpret_cast<const double*>(&c->it->c_local),
@@ -600,6 +625,24 @@ int icp_hip_iterate(icp_hip_ctx* c, const double* T_apply, int iter, int rules, 
   }
   HIP_TRY(hipEventRecord(ev[2], s));
   c->n_iterates++;
+  c->have_prev = true;  // the next iterate's search guesses from this one's matches
+  if (seq_out) *seq_out = seq;
+  return ICP_HIP_OK;
+}
+
+extern "C" {
+
+int icp_hip_iterate(icp_hip_ctx* c, const double* T_apply, int iter, int rules, double sigma_multiplier,
+                    icp_iter_stats* out) {
+  if (!c || !out) return fail(ICP_HIP_EINVAL, "null argument");
+  if (c->group) return group_iterate(c, T_apply, iter, rules, sigma_multiplier, out);
+  if (!c->nodes) return fail(ICP_HIP_ENOTREADY, "target not set");
+  if (!c->x && c->n_src > 0) return fail(ICP_HIP_ENOTREADY, "source not set");
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  uint64_t seq = 0;
+  const int rc = enqueue_iterate(c, T_apply, T_apply != nullptr, iter, rules, sigma_multiplier, -1, &seq);
+  if (rc != ICP_HIP_OK) return rc;
   // The host's only wait of the iteration: the publishing kernel stores the record with
   // system-scope stores, waits for their acknowledgement, then stores the sequence word (no
   // fence; reduce_kernels.hip finalize_cov_publish). Polling the pinned word wakes the host within
@@ -644,9 +687,62 @@ int icp_hip_iterate(icp_hip_ctx* c, const double* T_apply, int iter, int rules, 
   out->n_lane_search = cert ? (int64_t)c->last_lists[2] : 0;
   out->n_ball_search = cert ? (int64_t)c->last_lists[1] : 0;
   c->have_results = true;
-  c->have_prev = true;
   return ICP_HIP_OK;
 }
+
+}  // extern "C"
+
+bool icp_hip_loop_eligible(const icp_hip_ctx* c) {
+  return c && !c->group && !c->xfn && c->cfg.device_loop && c->nodes && c->n_src > 0 && c->loopd;
+}
+
+int icp_hip_loop_run(icp_hip_ctx* c, icp::SessionCore* core, const icp::SessionParams* p, int rules, double sigma,
+                     int k, icp::LoopRec* recs, double* step_ms) {
+  if (!icp_hip_loop_eligible(c) || !core || !p || !recs || k < 0 || k > icp_hip_ctx::kLoopRing)
+    return fail(ICP_HIP_EINVAL, "device loop: bad arguments");
+  if (k == 0 || core->done) {
+    for (int j = 0; j < k; j++) recs[j].outcome = icp::kStepNone;
+    return ICP_HIP_OK;
+  }
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  c->h_loop->core = *core;
+  c->h_loop->p = *p;
+  HIP_TRY(hipMemcpyAsync(c->loopd, c->h_loop, sizeof(LoopDev), hipMemcpyHostToDevice, s));
+  HIP_TRY(hipEventRecord(c->ev_batch, s));
+  const int64_t first = c->n_iterates;
+  // Iteration j > 0 runs only if iteration j - 1 left the session going, i.e. produced a
+  // transform: its search applies it. The first applies the session's pending increment.
+  for (int j = 0; j < k; j++) {
+    const int rc = enqueue_iterate(c, nullptr, j > 0 || core->pending, core->iter + j, rules, sigma, j, nullptr);
+    if (rc != ICP_HIP_OK) return rc;
+  }
+  HIP_TRY(hipMemcpyAsync(c->h_loop, c->loopd, sizeof(LoopDev), hipMemcpyDeviceToHost, s));
+  const hipError_t e = hipStreamSynchronize(s);
+  if (e != hipSuccess) return fail(ICP_HIP_EDEVICE, std::string("device loop: ") + hipGetErrorString(e));
+  *core = c->h_loop->core;
+  std::memcpy(recs, c->h_ring, (size_t)k * sizeof(icp::LoopRec));
+  c->lists_zero = true;
+  c->have_results = true;
+  for (int j = k - 1; j >= 0; j--)
+    if (recs[j].outcome != icp::kStepNone) {
+      for (int q = 0; q < 3; q++) c->last_lists[q] = (unsigned int)recs[j].lists[q];
+      break;
+    }
+  if (step_ms) {
+    hipEvent_t prev = c->ev_batch;
+    for (int j = 0; j < k; j++) {
+      hipEvent_t end = c->ring[(first + j) % icp_hip_ctx::kTimingRing][2];
+      float ms = 0.f;
+      HIP_TRY(hipEventElapsedTime(&ms, prev, end));
+      step_ms[j] = ms;
+      prev = end;
+    }
+  }
+  return ICP_HIP_OK;
+}
+
+extern "C" {
 
 int icp_hip_debug_counters(icp_hip_ctx* c, uint64_t out[ICP_DBG_SLOTS]) {
   if (!c || !out) return fail(ICP_HIP_EINVAL, "null argument");

@@ -60,6 +60,15 @@ struct icp_hip_ctx {
   icp::IterDev* h_it = nullptr;      // pinned, coherent: the publishing kernel stores into it
   icp::IterDev* h_it_dev = nullptr;  // its device address
   uint64_t publish_seq = 0;          // h_it->pad[3] = seq once the record is complete
+
+  // the device-resident loop (icp_hip_loop_run): the session state on the device, its pinned
+  // staging copy, and one LoopRec per iteration of a batch (pinned, written by the last kernel)
+  static constexpr int kLoopRing = kTimingRing;
+  icp::LoopDev* loopd = nullptr;
+  icp::LoopDev* h_loop = nullptr;
+  icp::LoopRec* h_ring = nullptr;
+  icp::LoopRec* h_ring_dev = nullptr;
+  hipEvent_t ev_batch = nullptr;  // a batch's start (its first iteration's step time)
   unsigned long long* counters = nullptr;
 
   // multi-GPU (comm or xfn set: every iterate runs the all-gather + rank-order merge path)
@@ -78,6 +87,16 @@ struct icp_hip_ctx {
 };
 
 void icp_ctx_set_error(const char* msg);
+
+// The device-resident loop: k iterations (k <= kLoopRing) enqueued back to back, each one's last
+// kernel stepping the session on the device (session_step.h), one host wait per batch. core is
+// the session state (uploaded, then updated), recs gets the k iterations' records (outcome
+// kStepNone once the session finished), step_ms (optional) each iteration's device time.
+// Eligible: a single-device context (RCCL communicator or none; not the host exchange) with
+// config.device_loop set.
+bool icp_hip_loop_eligible(const icp_hip_ctx* c);
+int icp_hip_loop_run(icp_hip_ctx* c, icp::SessionCore* core, const icp::SessionParams* p, int rules, double sigma,
+                     int k, icp::LoopRec* recs, double* step_ms);
 // Attach a communicator created elsewhere (ncclCommInitAll of a multi-device context); the
 // context owns it from then on.
 int icp_ctx_attach_comm(icp_hip_ctx* c, ncclComm_t comm, int nranks, int rank);

@@ -8,8 +8,17 @@
 
 #include "../../include/icp_hip.h"
 #include "icp_common.h"
+#include "session_step.h"
 
 namespace icp {
+
+// The device-resident loop's state (device memory): the session (engine.cpp's decisions,
+// session_step.h) stepped by each iteration's last kernel; every kernel of a later iteration
+// reads `done` and returns at once after the session finished, and the search applies core.T.
+struct LoopDev {
+  SessionCore core;
+  SessionParams p;
+};
 
 // Per-iteration record. Device-resident copy written by the merge/finalize kernels (the cull
 // kernel reads the threshold from it); the last kernel of the iteration stores the finished
@@ -37,6 +46,7 @@ struct WaveBox {
 };
 
 struct NNLaunch {
+  const LoopDev* loop;      // device loop (null: the host drives the iterate); T from loop->core.T
   const NodeRec* nodes;
   const TgtPt* pts;
   double* x;
@@ -88,6 +98,7 @@ hipError_t launch_nn(const NNLaunch& a, hipStream_t s);
 hipError_t launch_target_sep(const NodeRec* nodes, TgtPt* pts, int64_t n, int levels, hipStream_t s);
 
 struct CullLaunch {
+  const LoopDev* loop;  // device loop: nothing to do once the session is done
   const double* x;
   const double* y;
   const double* z;
@@ -100,7 +111,7 @@ struct CullLaunch {
 
 // Residual moments of the settled queries in fixed parts (deterministic), then the merges.
 int64_t moments_num_parts(int64_t n);
-hipError_t launch_moments(const double* dist, int64_t n, Moments* part, hipStream_t s);
+hipError_t launch_moments(const double* dist, int64_t n, Moments* part, const LoopDev* loop, hipStream_t s);
 // Partial buffers need merge_scratch_entries(nparts) entries of fold scratch behind the partials.
 int64_t merge_scratch_entries(int64_t nparts);
 
@@ -123,6 +134,10 @@ struct IterPublish {
   IterDev* host;
   unsigned int* lists;
   double seq;  // stored last into host->pad[3]: the record is complete
+  // device loop (host null): the session steps on the device and the iteration's LoopRec goes
+  // to `rec` (pinned host memory, read after the batch)
+  LoopDev* loop;
+  LoopRec* rec;
 };
 
 

@@ -250,9 +250,10 @@ __device__ __forceinline__ void load_query(const NNLaunch& a, int64_t i, bool ac
   qy = a.y[i];
   qz = a.z[i];
   if (APPLY) {
-    const double nx = ((a.T[0] * qx + a.T[1] * qy) + a.T[2] * qz) + a.T[3];
-    const double ny = ((a.T[4] * qx + a.T[5] * qy) + a.T[6] * qz) + a.T[7];
-    const double nz = ((a.T[8] * qx + a.T[9] * qy) + a.T[10] * qz) + a.T[11];
+    const double* T = a.loop ? a.loop->core.T : a.T;  // the device loop's pending increment
+    const double nx = ((T[0] * qx + T[1] * qy) + T[2] * qz) + T[3];
+    const double ny = ((T[4] * qx + T[5] * qy) + T[6] * qz) + T[7];
+    const double nz = ((T[8] * qx + T[9] * qy) + T[10] * qz) + T[11];
     a.x[i] = nx;
     a.y[i] = ny;
     a.z[i] = nz;
@@ -273,9 +274,10 @@ __device__ __forceinline__ void load_query32(const NNLaunch& a, int32_t i, bool 
   qy = qat(a.y, i);
   qz = qat(a.z, i);
   if (APPLY) {
-    const double nx = ((a.T[0] * qx + a.T[1] * qy) + a.T[2] * qz) + a.T[3];
-    const double ny = ((a.T[4] * qx + a.T[5] * qy) + a.T[6] * qz) + a.T[7];
-    const double nz = ((a.T[8] * qx + a.T[9] * qy) + a.T[10] * qz) + a.T[11];
+    const double* T = a.loop ? a.loop->core.T : a.T;  // the device loop's pending increment
+    const double nx = ((T[0] * qx + T[1] * qy) + T[2] * qz) + T[3];
+    const double ny = ((T[4] * qx + T[5] * qy) + T[6] * qz) + T[7];
+    const double nz = ((T[8] * qx + T[9] * qy) + T[10] * qz) + T[11];
     qx = nx;
     qy = ny;
     qz = nz;

@@ -64,6 +64,7 @@ using namespace dev;
 // The reference-order kernel.
 template <bool APPLY, bool COUNT>
 __global__ void __launch_bounds__(256) k_nn_ref(NNLaunch a) {
+  if (a.loop && a.loop->core.done) return;  // the device loop's session finished
   extern __shared__ __attribute__((aligned(16))) unsigned long long lds_stack[];
   const int bs = blockDim.x;
   const int64_t i = (int64_t)blockIdx.x * bs + threadIdx.x;
@@ -972,6 +973,7 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
 
 template <bool APPLY, int NG, bool CERT>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) k_nn_wave(NNLaunch a) {
+  if (a.loop && a.loop->core.done) return;  // the device loop's session finished
   extern __shared__ __attribute__((aligned(16))) unsigned long long lds_raw[];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int32_t i = (int32_t)(xcd_block((unsigned)a.xcd_blocks) * blockDim.x + threadIdx.x);  // n <= INT32_MAX
@@ -982,6 +984,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
 // the list is complete when this kernel starts), lanes 0..31 each one query.
 template <int NG>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) k_nn_half(NNLaunch a) {
+  if (a.loop && a.loop->core.done) return;
   extern __shared__ __attribute__((aligned(16))) unsigned long long lds_raw[];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   unsigned char* wl = reinterpret_cast<unsigned char*>(lds_raw) + wv * kWaveLds;
@@ -1043,6 +1046,7 @@ __device__ __forceinline__ void lane_query(const NNLaunch& a, int64_t i, unsigne
 }
 
 __global__ void __launch_bounds__(64) k_nn_ball(NNLaunch a) {
+  if (a.loop && a.loop->core.done) return;
   extern __shared__ __attribute__((aligned(16))) unsigned long long lds_raw[];
   const int lane = threadIdx.x, g = lane / kBallGL, gl = lane % kBallGL, gbase = g * kBallGL;
   int32_t* stack = reinterpret_cast<int32_t*>(lds_raw) + g * kBallGStack;

@@ -129,7 +129,9 @@ __device__ void cov_shift_store(const double* x, const double* y, const double* 
 constexpr int kMomPer = 16;
 constexpr int kMomPart = 256 * kMomPer;
 
-__global__ void __launch_bounds__(256) k_moments(const double* __restrict__ dist, int64_t n, MomSums* part) {
+__global__ void __launch_bounds__(256) k_moments(const double* __restrict__ dist, int64_t n, MomSums* part,
+                                                const LoopDev* loop) {
+  if (loop && loop->core.done) return;  // the device loop's session finished (block-uniform)
   __shared__ double red[4 * 4];
   const double c = moment_shift_block(dist, n, red);
   const int64_t b0 = (int64_t)blockIdx.x * kMomPart + threadIdx.x;
@@ -271,6 +273,43 @@ __global__ void __launch_bounds__(64) k_finalize_moments(const Moments* gathered
   cov_shift_store(cl.x, cl.y, cl.z, cl.pos, cl.pts, cl.n, thr_s, it);
 }
 
+// The device loop's step (one thread): the session's decisions on this iteration's finished
+// record (session_step.h, the host loop's own function), then the iteration's LoopRec into pinned
+// host memory (plain stores: the host reads it after synchronizing the stream).
+__device__ void loop_step(LoopDev* L, const IterDev& r, LoopRec* out) {
+  // fields stored one by one (a local LoopRec would live in scratch)
+  out->n = r.m_global.n;
+  out->mean = r.mean;
+  out->sd = r.sd;
+  out->thr = r.thr;
+  out->valid = r.c_global.n;
+  out->rmse = r.rmse;
+  out->sum_d2 = r.c_global.sum_d2;
+  out->dmin = r.m_global.dmin;
+  out->dmax = r.m_global.dmax;
+  out->nbad = r.m_global.nbad;
+  for (int k = 0; k < 3; k++) {
+    out->ma[k] = r.c_global.ma[k];
+    out->mb[k] = r.c_global.mb[k];
+    out->lists[k] = r.pad[k];
+  }
+  for (int k = 0; k < 9; k++) out->H[k] = r.c_global.c[k];
+  SessionCore core = L->core;
+  out->iter = core.iter;
+  int32_t outcome = kStepNone;  // enqueued past the end of the session: nothing ran
+  if (!core.done) {
+    core.pending = 0;  // this iteration's search applied the pending increment
+    outcome = session_core_step(core, L->p, r.rmse, (int64_t)r.c_global.n, r.c_global.ma, r.c_global.mb,
+                                r.c_global.c);
+    L->core = core;
+  }
+  out->outcome = outcome;
+  for (int k = 0; k < 16; k++) {
+    out->T[k] = core.T[k];
+    out->Tc[k] = core.Tc[k];
+  }
+}
+
 // The iteration's record goes straight into the caller's pinned host buffer (no copy engine or
 // blit launch on the critical path): the block copies the device record to LDS, thread 0
 // completes it, the block stores it with system-scope relaxed stores, every thread waits for its
@@ -294,7 +333,9 @@ __device__ void finalize_cov_publish(IterDev* it, const CovMoments& g, IterPubli
     for (int k = 0; k < 5; k++) pub.lists[k] = 0u;  // + the half list of the wave search
     it->c_global = rec->c_global;
     it->rmse = rec->rmse;
+    if (pub.loop) loop_step(pub.loop, *rec, pub.rec);
   }
+  if (pub.loop) return;  // the device loop: the host reads the batch's records after it
   __syncthreads();
   double* dst = reinterpret_cast<double*>(pub.host);
   for (int k = threadIdx.x; k < kWords; k += blockDim.x)
@@ -353,6 +394,7 @@ __global__ void __launch_bounds__(64) k_finalize_cov(const CovMoments* gathered,
 constexpr int kCullPer = 4;
 
 __global__ void __launch_bounds__(256) k_cull_cov(CullLaunch a) {
+  if (a.loop && a.loop->core.done) return;  // the device loop's session finished (block-uniform)
   __shared__ double red[4 * 17];
   const double thr = a.it->thr;
   double sh[6];
@@ -445,10 +487,10 @@ int64_t merge_scratch_entries(int64_t nparts) {
 
 int64_t moments_num_parts(int64_t n) { return (n + kMomPart - 1) / kMomPart; }
 
-hipError_t launch_moments(const double* dist, int64_t n, Moments* part, hipStream_t s) {
+hipError_t launch_moments(const double* dist, int64_t n, Moments* part, const LoopDev* loop, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_moments, dim3((unsigned)moments_num_parts(n)), dim3(256), 0, s, dist, n,
-                     reinterpret_cast<MomSums*>(part));
+                     reinterpret_cast<MomSums*>(part), loop);
   return hipGetLastError();
 }
 
@@ -480,7 +522,7 @@ hipError_t launch_merge_cov(const CovMoments* part, int64_t nparts, const CullLa
   const CovSums* cur = merge_to_last_span<CovSums, covsum_merge, covsum_identity>(
       reinterpret_cast<const CovSums*>(part), &nparts, s);
   hipLaunchKernelGGL(k_merge_cov_last, dim3(1), dim3(256), 0, s, cur, nparts, cl, it,
-                     pub ? *pub : IterPublish{nullptr, nullptr, 0.0}, pub ? 1 : 0);
+                     pub ? *pub : IterPublish{nullptr, nullptr, 0.0, nullptr, nullptr}, pub ? 1 : 0);
   return hipGetLastError();
 }
 

@@ -102,7 +102,11 @@ ICP_HD void jacobi_svd3(const double H[9], double U9[9], double S[3], double V9[
   // first index of a maximum, as Eigen's maxCoeff visitor (strict >)
   for (bool done = false; !done;) {
     done = true;
+    // (p, q) = (1, 0), (2, 0), (2, 1), unrolled: constant indices keep the matrices in registers
+    // on the device (a dynamic index puts them in scratch)
+#pragma unroll
     for (int p = 1; p < 3; p++) {
+#pragma unroll
       for (int q = 0; q < p; q++) {
         const double thr = smax(kDblMin, precision * max_diag);
         if (__builtin_fabs(w.a[p][q]) > thr || __builtin_fabs(w.a[q][p]) > thr) {
@@ -125,18 +129,35 @@ ICP_HD void jacobi_svd3(const double H[9], double U9[9], double S[3], double V9[
       for (int r = 0; r < 3; r++) u.a[r][i] = -u.a[r][i];
   }
   for (int i = 0; i < 3; i++) S[i] *= scale;
-  for (int i = 0; i < 3; i++) {
+  // selection sort, descending: at step i the first index of the maximum of S[i..2] (strict >)
+  // is swapped in; a zero maximum ends it (Eigen's JacobiSVD). Written with constant indices
+  // (each swap candidate tested in turn) so that nothing is indexed dynamically.
+  bool sorted_end = false;
+#pragma unroll
+  for (int i = 0; i < 2; i++) {
+    if (sorted_end) break;
     int pos = i;
+    double best = S[i];
+#pragma unroll
     for (int k = i + 1; k < 3; k++)
-      if (S[k] > S[pos]) pos = k;
-    if (S[pos] == 0.0) break;
-    if (pos != i) {
-      double t = S[i]; S[i] = S[pos]; S[pos] = t;
-      for (int r = 0; r < 3; r++) {
-        t = u.a[r][i]; u.a[r][i] = u.a[r][pos]; u.a[r][pos] = t;
-        t = v.a[r][i]; v.a[r][i] = v.a[r][pos]; v.a[r][pos] = t;
+      if (S[k] > best) {
+        pos = k;
+        best = S[k];
       }
+    if (best == 0.0) {
+      sorted_end = true;
+      break;
     }
+#pragma unroll
+    for (int k = i + 1; k < 3; k++)
+      if (pos == k) {
+        double t = S[i]; S[i] = S[k]; S[k] = t;
+#pragma unroll
+        for (int r = 0; r < 3; r++) {
+          t = u.a[r][i]; u.a[r][i] = u.a[r][k]; u.a[r][k] = t;
+          t = v.a[r][i]; v.a[r][i] = v.a[r][k]; v.a[r][k] = t;
+        }
+      }
   }
   for (int i = 0; i < 3; i++)
     for (int j = 0; j < 3; j++) {
