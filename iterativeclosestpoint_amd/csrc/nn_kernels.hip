@@ -19,6 +19,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstddef>
+#include <type_traits>
 
 #include "kernels.h"
 #include "nn_device.h"
@@ -196,8 +197,11 @@ __device__ __forceinline__ unsigned xcd_block(unsigned chunk) {
 // The search of one wave's queries (query i per lane; i >= n: an idle lane). HALF: the second
 // pass over the 32-query halves of the waves whose box overflowed (k_nn_half: queries already
 // moved, no candidate cache; lanes 32..63 idle).
-template <bool APPLY, int NG, bool CERT, bool HALF>
+// DBG: the instance of a context with debug counters (ICP_DBG_* slots); the product instances
+// carry none of their code.
+template <bool APPLY, int NG, bool CERT, bool HALF, bool DBG>
 __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, const int lane, unsigned char* wl) {
+  constexpr bool kDbg = DBG && kDbgCounts;
   static_assert(NG == 1 || NG == 2 || NG == 4, "scan groups: 1, 2 or 4");
   static_assert(!(HALF && (APPLY || CERT)), "the half pass searches moved queries");
   const bool active = i < a.n;
@@ -288,7 +292,7 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
   //      the ball search (with u as their guess) and ends here, otherwise it searches them (2)
   if (CERT && a.have_prev) {
     const unsigned long long open = __ballot(active && !safe);
-    if (kDbgCounts && a.dbg) {
+    if (kDbg && a.dbg) {
       const unsigned long long settled = __ballot(safe);  // every lane takes part in the ballot
       if (lane == 0) {
         atomicAdd(&a.dbg[19], (unsigned long long)__popcll(settled));
@@ -401,7 +405,7 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
       int tail = 1;
       if (a.cells) {
         tail = cell_starts<64, kWaveStartK>(a, wlx, wly, wlz, whx, why, whz, lane, 0, queue);
-        if (kDbgCounts && a.dbg && lane == 0) atomicAdd(&a.dbg[21], (unsigned long long)tail);
+        if (kDbg && a.dbg && lane == 0) atomicAdd(&a.dbg[21], (unsigned long long)tail);
       } else {
         // Wave-uniform descent to the deepest node that holds every leaf meeting B: follow the
         // only child meeting B while there is exactly one.
@@ -416,7 +420,7 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
           if (__builtin_popcount(kids) != 1) break;
           const uint32_t o = (uint32_t)__builtin_ctz(kids);
           start = __builtin_amdgcn_readfirstlane(topo.x + __builtin_popcount((meta & 0xffu) & ((1u << o) - 1u)));
-          if (kDbgCounts && a.dbg && lane == 0) atomicAdd(&a.dbg[21], 1ull);
+          if (kDbg && a.dbg && lane == 0) atomicAdd(&a.dbg[21], 1ull);
         }
         if (lane == 0) queue[0] = start;
       }
@@ -477,7 +481,7 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
           queue[off++] = first1 + __builtin_popcount(meta1 & 0xffu & ((1u << o) - 1u));
         }
         tail += tot;
-        if (kDbgCounts && a.dbg && lane == 0) atomicAdd(&a.dbg[5], 1ull);
+        if (kDbg && a.dbg && lane == 0) atomicAdd(&a.dbg[5], 1ull);
         wave_lds_fence();
       }
   };
@@ -507,7 +511,7 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
         fhx = hhx;
         fhy = hhy;
         fhz = hhz;
-        if (kDbgCounts && a.dbg && lane == 0) atomicAdd(&a.dbg[12], 1ull);
+        if (kDbg && a.dbg && lane == 0) atomicAdd(&a.dbg[12], 1ull);
       }
     }
     if (!reuse) {
@@ -560,7 +564,7 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
       wb->count = count;
       wb->gen = a.wc_gen;
     }
-    if (kDbgCounts && a.dbg && lane == 0) atomicAdd(&a.dbg[13], 1ull);
+    if (kDbg && a.dbg && lane == 0) atomicAdd(&a.dbg[13], 1ull);
   };
   // An overflowing wave (its box holds more candidates than the list takes): its joined queries
   // are searched again as two 32-query halves (k_nn_half), each with the smaller box of its own
@@ -583,12 +587,12 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
           a.fb_list3[2 * at] = (int32_t)(2 * wid + 1);
           a.fb_list3[2 * at + 1] = (int32_t)(uint32_t)(dm >> 32);
         }
-        if (kDbgCounts && a.dbg) atomicAdd(&a.dbg[16], (unsigned long long)nh);
+        if (kDbg && a.dbg) atomicAdd(&a.dbg[16], (unsigned long long)nh);
       }
     }
     join = false;
   }
-  if (kDbgCounts && a.dbg && lane == 0) {
+  if (kDbg && a.dbg && lane == 0) {
     atomicAdd(&a.dbg[0], 1ull);
     if (overflow) atomicAdd(&a.dbg[1], 1ull);
   }
@@ -729,7 +733,7 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
           // lockstep over this group's staged pairs (each group's 16-B reads broadcast)
           const float k1_in = k1;
           const int mp = len >> 1;
-          if (kDbgCounts && a.dbg && lane == 0) {
+          if (kDbg && a.dbg && lane == 0) {
             atomicAdd(&a.dbg[9], (unsigned long long)(maxc - r0 < S ? maxc - r0 : S));
             atomicAdd(&a.dbg[10], (unsigned long long)mp);
             atomicAdd(&a.dbg[11], 1ull);
@@ -838,7 +842,7 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
     wstore = false;
   }
   if (need64) {
-    if (kDbgCounts && a.dbg && lane == 0) atomicAdd(&a.dbg[8], 1ull);
+    if (kDbg && a.dbg && lane == 0) atomicAdd(&a.dbg[8], 1ull);
     // Points outside B are farther than r from every joined lane (each ball lies in B), so
     // they can neither be a joined lane's nearest point nor sit in its certificate window.
     // Exact duplicates of the winner (identical coordinates) are not ties: they share its leaf
@@ -913,9 +917,9 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
       store_header(wcount);
       wstore = false;
     }
-    if (kDbgCounts && a.dbg && lane == 0) atomicAdd(&a.dbg[4], (unsigned long long)scanned_pts);
+    if (kDbg && a.dbg && lane == 0) atomicAdd(&a.dbg[4], (unsigned long long)scanned_pts);
   }
-  if (kDbgCounts && a.dbg) {
+  if (kDbg && a.dbg) {
     const unsigned long long ex = __ballot(cand && !join && !overflow);
     const unsigned long long cov = __ballot(join && !(best <= u));
     const unsigned long long nc = __ballot(active && finite_q && !safe && !cand);
@@ -971,18 +975,18 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
 #endif
 }
 
-template <bool APPLY, int NG, bool CERT>
+template <bool APPLY, int NG, bool CERT, bool DBG>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) k_nn_wave(NNLaunch a) {
   if (a.loop && a.loop->core.done) return;  // the device loop's session finished
   extern __shared__ __attribute__((aligned(16))) unsigned long long lds_raw[];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int32_t i = (int32_t)(xcd_block((unsigned)a.xcd_blocks) * blockDim.x + threadIdx.x);  // n <= INT32_MAX
-  wave_search<APPLY, NG, CERT, false>(a, i, lane, reinterpret_cast<unsigned char*>(lds_raw) + wv * kWaveLds);
+  wave_search<APPLY, NG, CERT, false, DBG>(a, i, lane, reinterpret_cast<unsigned char*>(lds_raw) + wv * kWaveLds);
 }
 
 // The half pass: every wave takes 32-query halves of overflowed waves from the list (grid-stride;
 // the list is complete when this kernel starts), lanes 0..31 each one query.
-template <int NG>
+template <int NG, bool DBG>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) k_nn_half(NNLaunch a) {
   if (a.loop && a.loop->core.done) return;
   extern __shared__ __attribute__((aligned(16))) unsigned long long lds_raw[];
@@ -996,7 +1000,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
     const int64_t q = (int64_t)hb * 32 + lane;
     const int32_t i = (lane < 32 && ((mask >> lane) & 1u) && q < a.n) ? (int32_t)q : (int32_t)a.n;
     wave_lds_fence();  // the previous half's LDS reads are done
-    wave_search<false, NG, false, true>(a, i, lane, wl);
+    wave_search<false, NG, false, true, DBG>(a, i, lane, wl);
   }
 }
 
@@ -1368,21 +1372,25 @@ hipError_t launch_nn(const NNLaunch& a, hipStream_t s) {
   };
   // the previous-match certificate only where it can apply (an iterate after a search)
   const bool cert = a.certify_prev != 0 && a.have_prev;
-  switch ((cert ? 16 : 0) + (a.apply ? 8 : 0) + a.scan_groups) {
-    case 9: wave(k_nn_wave<true, 1, false>); break;
-    case 10: wave(k_nn_wave<true, 2, false>); break;
-    case 12: wave(k_nn_wave<true, 4, false>); break;
-    case 1: wave(k_nn_wave<false, 1, false>); break;
-    case 2: wave(k_nn_wave<false, 2, false>); break;
-    case 4: wave(k_nn_wave<false, 4, false>); break;
-    case 16 + 9: wave(k_nn_wave<true, 1, true>); break;
-    case 16 + 10: wave(k_nn_wave<true, 2, true>); break;
-    case 16 + 12: wave(k_nn_wave<true, 4, true>); break;
-    case 16 + 1: wave(k_nn_wave<false, 1, true>); break;
-    case 16 + 2: wave(k_nn_wave<false, 2, true>); break;
-    case 16 + 4: wave(k_nn_wave<false, 4, true>); break;
-    default: return hipErrorInvalidValue;
-  }
+  // instances: transform, scan groups, certificate, debug counters
+  auto pick = [&](auto cert_c, auto dbg_c) -> hipError_t {
+    constexpr bool C = decltype(cert_c)::value, D = decltype(dbg_c)::value;
+    switch ((a.apply ? 8 : 0) + a.scan_groups) {
+      case 9: wave(k_nn_wave<true, 1, C, D>); break;
+      case 10: wave(k_nn_wave<true, 2, C, D>); break;
+      case 12: wave(k_nn_wave<true, 4, C, D>); break;
+      case 1: wave(k_nn_wave<false, 1, C, D>); break;
+      case 2: wave(k_nn_wave<false, 2, C, D>); break;
+      case 4: wave(k_nn_wave<false, 4, C, D>); break;
+      default: return hipErrorInvalidValue;
+    }
+    return hipSuccess;
+  };
+  using T_ = std::true_type;
+  using F_ = std::false_type;
+  const bool dbg = a.dbg != nullptr;
+  const hipError_t pe = cert ? (dbg ? pick(T_{}, T_{}) : pick(T_{}, F_{})) : (dbg ? pick(F_{}, T_{}) : pick(F_{}, F_{}));
+  if (pe != hipSuccess) return pe;
   // the half pass over the overflowed waves (queries already moved: no transform, no cache)
   if (a.fb_list3) {
     NNLaunch h = a;
@@ -1392,10 +1400,13 @@ hipError_t launch_nn(const NNLaunch& a, hipStream_t s) {
     const int64_t halves = (a.n + 31) / 32;
     const int64_t hb = (halves + 3) / 4;
     const unsigned hgrid = (unsigned)(hb < 2048 ? hb : 2048);  // about one resident block per slot
-    switch (a.scan_groups) {
-      case 1: hipLaunchKernelGGL(k_nn_half<1>, dim3(hgrid), dim3(256), wshm, s, h); break;
-      case 2: hipLaunchKernelGGL(k_nn_half<2>, dim3(hgrid), dim3(256), wshm, s, h); break;
-      case 4: hipLaunchKernelGGL(k_nn_half<4>, dim3(hgrid), dim3(256), wshm, s, h); break;
+    switch (a.scan_groups + (dbg ? 8 : 0)) {
+      case 1: hipLaunchKernelGGL((k_nn_half<1, false>), dim3(hgrid), dim3(256), wshm, s, h); break;
+      case 2: hipLaunchKernelGGL((k_nn_half<2, false>), dim3(hgrid), dim3(256), wshm, s, h); break;
+      case 4: hipLaunchKernelGGL((k_nn_half<4, false>), dim3(hgrid), dim3(256), wshm, s, h); break;
+      case 9: hipLaunchKernelGGL((k_nn_half<1, true>), dim3(hgrid), dim3(256), wshm, s, h); break;
+      case 10: hipLaunchKernelGGL((k_nn_half<2, true>), dim3(hgrid), dim3(256), wshm, s, h); break;
+      case 12: hipLaunchKernelGGL((k_nn_half<4, true>), dim3(hgrid), dim3(256), wshm, s, h); break;
       default: return hipErrorInvalidValue;
     }
   }
