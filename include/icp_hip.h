@@ -104,7 +104,12 @@ typedef struct icp_hip_config {
                              lane's fp64 Jacobi SVD, ~8.5 us) costs what the host round trip
                              does (7-11 us): equal at 10M and 1.25M shards, 5 % slower at 100k
                                                                             dflt 0 */
-  int32_t reserved[3];    /* zero */
+  int32_t timing_stride;  /* iterates whose search kernel is timed by events on its dispatch and the
+                             next kernel's (icp_hip_timings): every timing_stride-th iterate of the
+                             context (the first included); 0: none. An event on a dispatch packet
+                             delays the next kernel by ~3-5 us (every iterate timed: config 2,
+                             100k, 12-15 % slower)                                      dflt 0 */
+  int32_t reserved[2];    /* zero */
 } icp_hip_config;
 
 /* Slots of icp_hip_debug_counters (summed over the last iterate's search launches). */
@@ -277,7 +282,8 @@ int icp_hip_target_info(icp_hip_ctx* ctx, int64_t* n_nodes, int64_t* n_leaves, i
  * whole device part of the last iterate. */
 int icp_hip_last_timing(icp_hip_ctx* ctx, double* nn_kernel_ms, double* iterate_device_ms);
 
-/* The same for each of the last k iterates (k <= 256, the context's timing ring), oldest first.
+/* The same for each of the last k iterates (k <= 256, the context's timing ring), oldest first;
+ * NaN for an iterate that config.timing_stride left untimed.
  * Waits for them to finish. */
 int icp_hip_timings(icp_hip_ctx* ctx, int k, double* nn_kernel_ms, double* iterate_device_ms);
 

@@ -146,6 +146,7 @@ void icp_hip_config_default(icp_hip_config* cfg) {
   cfg->candidate_margin = 16;
   cfg->overflow_halves = 1;
   cfg->device_loop = 0;
+  cfg->timing_stride = 0;
 }
 
 int icp_hip_create(icp_hip_ctx** out, int device) { return icp_hip_create_ex(out, device, nullptr); }
@@ -170,6 +171,7 @@ int icp_hip_create_ex(icp_hip_ctx** out, int device, const icp_hip_config* cfg) 
   if (conf.query_order != 0 && conf.query_order != 1) return fail(ICP_HIP_EINVAL, "config: query_order must be 0 or 1");
   if (conf.certify_prev < 0 || conf.certify_prev > 3) return fail(ICP_HIP_EINVAL, "config: certify_prev out of [0, 3]");
   if (conf.device_loop != 0 && conf.device_loop != 1) return fail(ICP_HIP_EINVAL, "config: device_loop must be 0 or 1");
+  if (conf.timing_stride < 0) return fail(ICP_HIP_EINVAL, "config: timing_stride must be >= 0");
   if (!(conf.join_factor >= 1.0 && conf.join_factor <= 1e6))
     return fail(ICP_HIP_EINVAL, "config: join_factor out of [1, 1e6]");
   int ndev = 0;
@@ -579,8 +581,12 @@ static int enqueue_iterate(icp_hip_ctx* c, const double* T_apply, bool apply, in
   if (!c->lists_zero) HIP_TRY(hipMemsetAsync(c->fb_count, 0, 8 * sizeof(unsigned int), s));
   c->lists_zero = false;
   if (c->dbg) HIP_TRY(hipMemsetAsync(c->dbg, 0, ICP_DBG_SLOTS * sizeof(unsigned long long), s));
-  a.ev_start = ev[0];
-  a.ev_fast_done = ev[1];
+  // the search's timing events (on dispatch packets) on every timing_stride-th iterate only
+  const int64_t slot = c->n_iterates % icp_hip_ctx::kTimingRing;
+  const bool timed = c->cfg.timing_stride > 0 && c->n_iterates % c->cfg.timing_stride == 0;
+  c->timed[slot] = timed;
+  a.ev_start = timed ? ev[0] : nullptr;
+  a.ev_fast_done = timed ? ev[1] : nullptr;
   HIP_TRY(launch_nn(a, s));
   // residual moments -> mean, std, threshold (no communicator: fused into the last merge level)
   const bool multi = c->comm != nullptr || c->xfn != nullptr;
@@ -895,11 +901,17 @@ int icp_hip_timings(icp_hip_ctx* c, int k, double* nn_ms, double* it_ms) {
   if (k > icp_hip_ctx::kTimingRing || k > c->n_iterates) return fail(ICP_HIP_EINVAL, "fewer iterates recorded than asked");
   HIP_TRY(hipSetDevice(c->device));
   for (int j = 0; j < k; j++) {
-    hipEvent_t* ev = c->ring[(c->n_iterates - k + j) % icp_hip_ctx::kTimingRing];
+    const int64_t slot = (c->n_iterates - k + j) % icp_hip_ctx::kTimingRing;
+    hipEvent_t* ev = c->ring[slot];
     HIP_TRY(hipEventSynchronize(ev[2]));
-    float a = 0.f, b = 0.f;
-    HIP_TRY(hipEventElapsedTime(&a, ev[0], ev[1]));
-    HIP_TRY(hipEventElapsedTime(&b, ev[0], ev[2]));
+    double a = std::nan(""), b = std::nan("");
+    if (c->timed[slot]) {
+      float fa = 0.f, fb = 0.f;
+      HIP_TRY(hipEventElapsedTime(&fa, ev[0], ev[1]));
+      HIP_TRY(hipEventElapsedTime(&fb, ev[0], ev[2]));
+      a = fa;
+      b = fb;
+    }
     if (nn_ms) nn_ms[j] = a;
     if (it_ms) it_ms[j] = b;
   }

@@ -19,6 +19,7 @@ struct icp_hip_ctx {
   // [0] search start (the iterate's first launch), [1] search kernel done, [2] iterate end
   static constexpr int kTimingRing = 256;
   hipEvent_t ring[kTimingRing][3] = {};
+  bool timed[kTimingRing] = {};  // the slot's search carries events (config.timing_stride)
   int64_t n_iterates = 0;
 
   // target (replicated on every rank)

@@ -41,6 +41,10 @@
 #ifndef ICP_SCAN_UNROLL
 #define ICP_SCAN_UNROLL 1
 #endif
+// Timing: the search's end as its own dispatch's stop event (1) or the next kernel's start (0)
+#ifndef ICP_SEARCH_STOP_EVENT
+#define ICP_SEARCH_STOP_EVENT 1
+#endif
 #ifndef ICP_SKIP_PREV_GATHER
 #define ICP_SKIP_PREV_GATHER 0
 #endif
@@ -1366,10 +1370,21 @@ hipError_t launch_nn(const NNLaunch& a, hipStream_t s) {
   // wave search -> ball search -> per-lane search / exact DFS
   const unsigned wgrid = grid_for(a.n, 256);
   const size_t wshm = (size_t)(256 / 64) * kWaveLds;
-  // the kernel's own dispatch records the timing events (null events: a plain launch)
+  // The timing events ride on the search's own dispatch packet (no marker packets between
+  // kernels). An event on a dispatch delays the next kernel by ~3-5 us (its start event carried
+  // by the next kernel's dispatch instead measured no better), so the context times only every
+  // config.timing_stride-th iterate (null events: plain launches).
+#if ICP_SEARCH_STOP_EVENT
+  hipEvent_t next_start = nullptr;
   auto wave = [&](auto kern) {
     hipExtLaunchKernelGGL(kern, dim3(wgrid), dim3(256), (uint32_t)wshm, s, a.ev_start, a.ev_fast_done, 0u, a);
   };
+#else
+  hipEvent_t next_start = a.ev_fast_done;
+  auto wave = [&](auto kern) {
+    hipExtLaunchKernelGGL(kern, dim3(wgrid), dim3(256), (uint32_t)wshm, s, a.ev_start, nullptr, 0u, a);
+  };
+#endif
   // the previous-match certificate only where it can apply (an iterate after a search)
   const bool cert = a.certify_prev != 0 && a.have_prev;
   // instances: transform, scan groups, certificate, debug counters
@@ -1400,15 +1415,19 @@ hipError_t launch_nn(const NNLaunch& a, hipStream_t s) {
     const int64_t halves = (a.n + 31) / 32;
     const int64_t hb = (halves + 3) / 4;
     const unsigned hgrid = (unsigned)(hb < 2048 ? hb : 2048);  // about one resident block per slot
+    auto half = [&](auto kern) {
+      hipExtLaunchKernelGGL(kern, dim3(hgrid), dim3(256), (uint32_t)wshm, s, next_start, nullptr, 0u, h);
+    };
     switch (a.scan_groups + (dbg ? 8 : 0)) {
-      case 1: hipLaunchKernelGGL((k_nn_half<1, false>), dim3(hgrid), dim3(256), wshm, s, h); break;
-      case 2: hipLaunchKernelGGL((k_nn_half<2, false>), dim3(hgrid), dim3(256), wshm, s, h); break;
-      case 4: hipLaunchKernelGGL((k_nn_half<4, false>), dim3(hgrid), dim3(256), wshm, s, h); break;
-      case 9: hipLaunchKernelGGL((k_nn_half<1, true>), dim3(hgrid), dim3(256), wshm, s, h); break;
-      case 10: hipLaunchKernelGGL((k_nn_half<2, true>), dim3(hgrid), dim3(256), wshm, s, h); break;
-      case 12: hipLaunchKernelGGL((k_nn_half<4, true>), dim3(hgrid), dim3(256), wshm, s, h); break;
+      case 1: half(k_nn_half<1, false>); break;
+      case 2: half(k_nn_half<2, false>); break;
+      case 4: half(k_nn_half<4, false>); break;
+      case 9: half(k_nn_half<1, true>); break;
+      case 10: half(k_nn_half<2, true>); break;
+      case 12: half(k_nn_half<4, true>); break;
       default: return hipErrorInvalidValue;
     }
+    next_start = nullptr;
   }
   // the follow-up lists are short (the ball list ~0.1 % of the queries, the exact list usually
   // empty): one launch of 64-thread blocks, grid-stride over them; LDS for the group stacks and
@@ -1418,7 +1437,8 @@ hipError_t launch_nn(const NNLaunch& a, hipStream_t s) {
   if (bshm < (size_t)kBallLdsBytes) bshm = kBallLdsBytes;
   static_assert(kBallGPoints * 4 >= 64 * 8, "a group's DFS stack (stride 1) holds >= 64 levels");
   if (levels > kBallGPoints * 4 / 8) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_nn_ball, dim3((unsigned)(bq < 8192 ? bq : 8192)), dim3(64), bshm, s, a);
+  hipExtLaunchKernelGGL(k_nn_ball, dim3((unsigned)(bq < 8192 ? bq : 8192)), dim3(64), (uint32_t)bshm, s, next_start,
+                        nullptr, 0u, a);
   return hipGetLastError();
 }
 

@@ -28,7 +28,7 @@ for name, spec in workloads.items():
     for mode in (0, 1, 2, 3):
         out = {"workload": name, "n": n, "certify_prev": mode}
         for counters in (0, 1):
-            with icp.Context(0, icp.config(certify_prev=mode, debug_counters=counters)) as ctx:
+            with icp.Context(0, icp.config(certify_prev=mode, debug_counters=counters, timing_stride=1)) as ctx:
                 ctx.set_target(tgt, 10, 20, icp.RULES_ENGINE)
                 ctx.set_source(src)
                 sess = ctx.session(icp.params_default(max_iterations=iters, tolerance=0.0,

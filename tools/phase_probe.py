@@ -14,7 +14,7 @@ import iterativeclosestpoint_amd as icp  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 10_000_000
 tgt, src, _ = icp.synth_pair(n)
-with icp.Context(0, icp.config(debug_counters=1)) as ctx:
+with icp.Context(0, icp.config(debug_counters=1, timing_stride=1)) as ctx:
     ctx.set_target(tgt, 10, 20, icp.RULES_ENGINE)
     ctx.set_source(src)
     sess = ctx.session(icp.params_default(max_iterations=20, tolerance=1e-6, flags=icp.FLAG_NO_EARLY_STOP))

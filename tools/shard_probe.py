@@ -2,8 +2,8 @@
 full 10M target, rank 0's source shard (spatial: a kd-order range; SPATIAL=0: a plain range of the
 shuffled cloud). Estimates the strong-scaling floor of bench.py --gpus W. RCCL=1 runs the
 iterations over a 1-rank RCCL communicator: the multi-rank path (two ncclAllGather + rank-order
-device merges per iteration) without the network. DEVICE_LOOP=0 steps every iteration on the
-host (icp_hip_config.device_loop; default 1: the device-resident loop)."""
+device merges per iteration) without the network. DEVICE_LOOP=1 runs the device-resident loop
+(icp_hip_config.device_loop; default 0: the host steps every iteration)."""
 import json
 import os
 import sys
@@ -18,7 +18,7 @@ from bench import shard_range
 n = int(os.environ.get("N", "10000000"))
 worlds = [int(w) for w in (sys.argv[1] if len(sys.argv) > 1 else "1,2,4,8").split(",")]
 tgt, src, _ = icp.synth_pair(n)
-ctx = icp.Context(0, icp.config(device_loop=int(os.environ.get("DEVICE_LOOP", "1"))))
+ctx = icp.Context(0, icp.config(device_loop=int(os.environ.get("DEVICE_LOOP", "0")), timing_stride=1))
 ctx.set_target(tgt, 10, 20, icp.RULES_ENGINE)
 if os.environ.get("RCCL", "0") == "1":
     ctx.comm_init(1, 0, icp.Context.unique_id())
