@@ -45,6 +45,11 @@
 #ifndef ICP_SEARCH_STOP_EVENT
 #define ICP_SEARCH_STOP_EVENT 1
 #endif
+// The first iterate's guess: the nearest point of every leaf child of the descent leaf's parent
+// (1) or of the descent leaf alone (0)
+#ifndef ICP_DESCENT_SIBLINGS
+#define ICP_DESCENT_SIBLINGS 1
+#endif
 #ifndef ICP_SKIP_PREV_GATHER
 #define ICP_SKIP_PREV_GATHER 0
 #endif
@@ -251,16 +256,38 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
     const NodeRec* r0 = a.nodes;
     double lx = r0->lo[0], ly = r0->lo[1], lz = r0->lo[2], hx = r0->hi[0], hy = r0->hi[1], hz = r0->hi[2];
     int32_t node = 0;
+    int32_t pfirst = -1;  // the current node's parent: its first child record, child mask, the
+    uint32_t pmask = 0, po = 0;  // octant taken and its children's squared axis distances
+    double psx[2] = {0.0, 0.0}, psy[2] = {0.0, 0.0}, psz[2] = {0.0, 0.0};
+    auto scan_leaf = [&](int2 topo) {
+      const int32_t cnt = (int32_t)((uint32_t)topo.y & ~kLeafBit);
+      for (int32_t k = 0; k < cnt; k++) {
+        const TgtPt* p = a.pts + topo.x + k;
+        const double dx = p->x - qx, dy = p->y - qy, dz = p->z - qz;
+        const double d2 = dx * dx + dy * dy + dz * dz;
+        u = d2 < u ? d2 : u;
+      }
+    };
     while (true) {
       const int2 topo = *reinterpret_cast<const int2*>(&a.nodes[node].first);
       const uint32_t meta = (uint32_t)topo.y;
       if (meta & kLeafBit) {
-        const int32_t cnt = (int32_t)(meta & ~kLeafBit);
-        for (int32_t k = 0; k < cnt; k++) {
-          const TgtPt* p = a.pts + topo.x + k;
-          const double dx = p->x - qx, dy = p->y - qy, dz = p->z - qz;
-          const double d2 = dx * dx + dy * dy + dz * dz;
-          u = d2 < u ? d2 : u;
+        scan_leaf(topo);
+        // (in the instances without a transform: a session's first iterate; the steady-state
+        // instances keep their registers for the scan)
+        if (ICP_DESCENT_SIBLINGS && !APPLY && pfirst >= 0) {
+          // then the points of the parent's other leaf children whose box is nearer than the
+          // best so far (~3 points per leaf: the reached leaf alone bounds the nearest distance
+          // loosely, and the first iterate's boxes, overflows and ball searches grow with it)
+#pragma unroll
+          for (int o = 0; o < 8; o++) {
+            const double c = psx[o & 1] + psy[(o >> 1) & 1] + psz[o >> 2];
+            if (((pmask >> o) & 1u) && (uint32_t)o != po && c < u) {
+              const int2 t =
+                  *reinterpret_cast<const int2*>(&a.nodes[pfirst + __builtin_popcount(pmask & ((1u << o) - 1u))].first);
+              if ((uint32_t)t.y & kLeafBit) scan_leaf(t);
+            }
+          }
         }
         break;
       }
@@ -282,6 +309,15 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
         o1 = take ? (uint32_t)o : o1;
       }
       node = topo.x + __builtin_popcount(mask & ((1u << o1) - 1u));
+      pfirst = topo.x;
+      pmask = mask;
+      po = o1;
+#pragma unroll
+      for (int k = 0; k < 2; k++) {
+        psx[k] = sx[k];
+        psy[k] = sy[k];
+        psz[k] = sz[k];
+      }
       if (o1 & 1u) lx = mx; else hx = mx;
       if (o1 & 2u) ly = my; else hy = my;
       if (o1 & 4u) lz = mz; else hz = mz;
