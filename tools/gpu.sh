@@ -5,7 +5,8 @@
 #   bash tools/gpu.sh round TAG              -m gpu suite, a default bench line, rocprof trace + PMC
 #   bash tools/gpu.sh ab TAG KEXPR REPS ARM...   optional tests (pytest -k KEXPR, "" none, "all"),
 #                                            then REPS interleaved bench lines per ARM
-#                                            (ARM = LIB[:key=val,...], LIB = a .so path or "cur")
+#                                            (ARM = LIB[:key=val,...], LIB = a .so path or "cur";
+#                                            AB_BENCH_ARGS: extra bench.py arguments, e.g. --points)
 #   bash tools/gpu.sh configs                bench lines of BASELINE configs 2, 3 (1 mm grid), 5
 #   bash tools/gpu.sh cfg5                   the 50M parity tests and a 50M bench line with parity
 #   bash tools/gpu.sh multi [PTS]            N > 1 rehearsals on one GPU: torchrun ranks over the host
@@ -62,7 +63,7 @@ ab)
       if [ "$ARM" != "$L" ]; then for kv in $(echo "${ARM#*:}" | tr ',' ' '); do CF="$CF --config $kv"; done; fi
       if [ "$L" = "cur" ]; then unset ICP_HIP_LIB; else export ICP_HIP_LIB=$PWD/$L; fi
       OUTF=gpurun_out/ab_$TAG.$r.$a.json
-      timeout -k 10 300 python3 bench.py --no-cpu-baseline --no-parity --no-registration $CF > $OUTF 2> gpurun_out/ab_$TAG.err || { tail -20 gpurun_out/ab_$TAG.err; exit 1; }
+      timeout -k 10 300 python3 bench.py --no-cpu-baseline --no-parity --no-registration $CF ${AB_BENCH_ARGS:-} > $OUTF 2> gpurun_out/ab_$TAG.err || { tail -20 gpurun_out/ab_$TAG.err; exit 1; }
       bench_line $OUTF "$ARM"
     done
   done
