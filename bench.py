@@ -270,6 +270,8 @@ def main() -> int:
     ap.add_argument("--no-parity", action="store_true",
                     help="skip the CPU checks (the timed state's correspondences and the fresh registration)")
     ap.add_argument("--no-registration", action="store_true", help="skip the stops-on registration leg")
+    ap.add_argument("--prewarm-ms", type=float, default=0.0,
+                    help="diagnostic: keep the GPU busy with a matrix loop this long before the warmup steps")
     ap.add_argument("--exchange", choices=("rccl", "host"), default="rccl",
                     help="per-iteration all-gathers: RCCL (default), or over torch.distributed gloo "
                          "through the host (rehearsal of N ranks on one GPU; RCCL refuses that)")
@@ -358,6 +360,14 @@ def main() -> int:
     params = icp.params_default(max_iterations=args.warmup + args.steps + 1, tolerance=1e-6,
                                 flags=icp.FLAG_NO_EARLY_STOP)
     sess = ctx.session(params)
+    if args.prewarm_ms > 0:
+        a_ = torch.randn(4096, 4096, device=f"cuda:{device}")
+        t_w = time.perf_counter()
+        while (time.perf_counter() - t_w) * 1e3 < args.prewarm_ms:
+            for _ in range(8):
+                a_ = torch.tanh(a_ @ a_)
+            torch.cuda.synchronize()
+        del a_
     # warmup; the first iteration (no previous residuals: the guess is a descent) is reported alone
     first_ms = sess.step_n_timed(1)
     first_nn_ms, _ = ctx.timings(1)

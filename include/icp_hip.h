@@ -109,7 +109,11 @@ typedef struct icp_hip_config {
                              context (the first included); 0: none. An event on a dispatch packet
                              delays the next kernel by ~3-5 us (every iterate timed: config 2,
                              100k, 12-15 % slower)                                      dflt 0 */
-  int32_t reserved[2];    /* zero */
+  int32_t candidate_loose; /* a cached candidate list is reused only while vol(B+) <= this / 100 x
+                              vol(B) (a wave whose box shrank walks again and stores a tighter
+                              list; the same results either way), in [100, 100000]; 0: the
+                              default                                                   dflt 190 */
+  int32_t reserved[1];    /* zero */
 } icp_hip_config;
 
 /* Slots of icp_hip_debug_counters (summed over the last iterate's search launches). */

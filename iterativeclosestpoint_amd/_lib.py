@@ -68,7 +68,7 @@ class HipConfig(C.Structure):
         ("xcd_blocks", C.c_int32), ("scan_groups", C.c_int32), ("candidate_cache", C.c_int32),
         ("candidate_margin", C.c_int32), ("certify_prev", C.c_int32), ("query_order", C.c_int32),
         ("overflow_halves", C.c_int32), ("device_loop", C.c_int32), ("timing_stride", C.c_int32),
-        ("reserved", C.c_int32 * 2),
+        ("candidate_loose", C.c_int32), ("reserved", C.c_int32 * 1),
     ]
 
 

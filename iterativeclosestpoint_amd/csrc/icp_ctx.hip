@@ -30,7 +30,6 @@ using namespace icp;
 
 // The candidate cache re-walks a wave whose stored box B+ has grown loose around its current B
 // (volume ratio; at 10M with margin 16: 1.4, 1.6 and 2.3 measured slower than 1.9).
-constexpr double kCacheLoose = 1.9;
 
 namespace {
 thread_local std::string g_err;
@@ -144,6 +143,7 @@ void icp_hip_config_default(icp_hip_config* cfg) {
   cfg->scan_groups = 2;
   cfg->candidate_cache = 1;
   cfg->candidate_margin = 16;
+  cfg->candidate_loose = 190;
   cfg->overflow_halves = 1;
   cfg->device_loop = 0;
   cfg->timing_stride = 0;
@@ -167,6 +167,9 @@ int icp_hip_create_ex(icp_hip_ctx** out, int device, const icp_hip_config* cfg) 
   if (conf.candidate_cache != 0 && conf.candidate_cache != 1) return fail(ICP_HIP_EINVAL, "config: candidate_cache must be 0 or 1");
   if (conf.candidate_margin < 0 || conf.candidate_margin > 1024)
     return fail(ICP_HIP_EINVAL, "config: candidate_margin out of [0, 1024]");
+  if (conf.candidate_loose == 0) conf.candidate_loose = 190;
+  if (conf.candidate_loose < 100 || conf.candidate_loose > 100000)
+    return fail(ICP_HIP_EINVAL, "config: candidate_loose out of [100, 100000]");
   if (conf.overflow_halves != 0 && conf.overflow_halves != 1) return fail(ICP_HIP_EINVAL, "config: overflow_halves must be 0 or 1");
   if (conf.query_order != 0 && conf.query_order != 1) return fail(ICP_HIP_EINVAL, "config: query_order must be 0 or 1");
   if (conf.certify_prev < 0 || conf.certify_prev > 3) return fail(ICP_HIP_EINVAL, "config: certify_prev out of [0, 3]");
@@ -577,7 +580,7 @@ static int enqueue_iterate(icp_hip_ctx* c, const double* T_apply, bool apply, in
   a.wc_ents = c->wc_ents;
   a.wc_gen = c->wc_gen;
   a.wc_margin = c->cfg.candidate_margin / 256.0;
-  a.wc_loose = kCacheLoose;
+  a.wc_loose = c->cfg.candidate_loose / 100.0;
   if (!c->lists_zero) HIP_TRY(hipMemsetAsync(c->fb_count, 0, 8 * sizeof(unsigned int), s));
   c->lists_zero = false;
   if (c->dbg) HIP_TRY(hipMemsetAsync(c->dbg, 0, ICP_DBG_SLOTS * sizeof(unsigned long long), s));
