@@ -135,6 +135,7 @@ typedef struct icp_hip_config {
 #define ICP_DBG_BALL_POINTS 15   /* points scanned by the ball search                          */
 #define ICP_DBG_HALVES 16        /* 32-query halves of overflowed waves searched again (k_nn_half) */
 #define ICP_DBG_CLK_GUESS 16     /* phase-clock build (-DICP_PHASE_CLOCKS=1), s_memtime: guess  */
+#define ICP_DBG_REUSED_ENTRIES 17 /* cache entries streamed by the waves that reused their record */
 #define ICP_DBG_CLK_BOX 17       /*                          search box                        */
 #define ICP_DBG_CLK_WALK 18      /*                          walk (cells + batches)            */
 #define ICP_DBG_CLK_SCAN 19      /*                          scan                              */

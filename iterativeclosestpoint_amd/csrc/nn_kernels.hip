@@ -551,7 +551,10 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
         fhx = hhx;
         fhy = hhy;
         fhz = hhz;
-        if (kDbg && a.dbg && lane == 0) atomicAdd(&a.dbg[12], 1ull);
+        if (kDbg && a.dbg && lane == 0) {
+          atomicAdd(&a.dbg[12], 1ull);
+          atomicAdd(&a.dbg[17], (unsigned long long)nleaf);  // entries a reusing wave streams
+        }
       }
     }
     if (!reuse) {
