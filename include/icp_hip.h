@@ -113,7 +113,12 @@ typedef struct icp_hip_config {
                               vol(B) (a wave whose box shrank walks again and stores a tighter
                               list; the same results either way), in [100, 100000]; 0: the
                               default                                                   dflt 190 */
-  int32_t reserved[1];    /* zero */
+  int32_t candidate_lead;  /* a walking wave of an iterate extends the B+ it stores, on each axis,
+                              by this many times the displacement of B's centre by the
+                              iterate's transform, on the side the queries moved to (ICP moves a
+                              wave's queries the same way for many iterates: a record then lasts
+                              until they have moved that far), in [0, 64]; 0: symmetric margin
+                              only                                                       dflt 8 */
 } icp_hip_config;
 
 /* Slots of icp_hip_debug_counters (summed over the last iterate's search launches). */
@@ -148,7 +153,10 @@ typedef struct icp_hip_config {
 #define ICP_DBG_START_NODES 21   /* start nodes taken from the cell tables / descent levels    */
 #define ICP_DBG_WINNER_PREV 22   /* winner-count build: joined lanes whose winner is the previous match */
 #define ICP_DBG_WINNER_LANES 23  /* winner-count build: joined lanes with an fp32 winner          */
-#define ICP_DBG_SLOTS 24
+#define ICP_DBG_WALK_MOVED 24   /* waves with a record of this generation that walked because
+                                    their box left B+                                        */
+#define ICP_DBG_WALK_LOOSE 25   /* waves whose box lay inside B+ but walked because B+ was loose */
+#define ICP_DBG_SLOTS 32
 
 typedef struct icp_hip_ctx icp_hip_ctx;
 
@@ -201,7 +209,15 @@ void icp_hip_destroy(icp_hip_ctx* ctx);
  * returned context as it accepts a single-device one: outputs in the caller's order, statistics
  * identical on all devices (those of a world of n_devices processes), timings the slowest
  * device's, search-path counts summed. comm_init / comm_init_host do not apply to it. A source
- * needs at least one point per device. n_devices = 1 with ICP_XPORT_AUTO gives a plain context. */
+ * needs at least one point per device (and fewer than 2^31 points in all). n_devices = 1 with
+ * ICP_XPORT_AUTO gives a plain context.
+ * Failures: a call that fails on one member returns that member's error (a peer's own
+ * ICP_HIP_EEXCHANGE is not reported over the root cause); the next call starts clean. Except:
+ * when an iterate fails over ICP_XPORT_RCCL, a peer may already have enqueued a collective that
+ * will never complete, so every member's communicator is aborted (ncclCommAbort: the pending
+ * collectives return) and the context is DEAD: every later call but icp_hip_destroy returns
+ * ICP_HIP_EDEVICE. Destroy it and create a new one. (Usage errors found before any member runs,
+ * e.g. no target or source, do not kill it.) */
 int icp_hip_create_multi(icp_hip_ctx** out, int n_devices, const int* device_ids, const icp_hip_config* cfg,
                          int transport);
 /* Devices (up to cap ids) and transport (ICP_XPORT_*) of a context. */
@@ -227,6 +243,13 @@ int icp_hip_comm_init(icp_hip_ctx* ctx, int nranks, int rank, const uint8_t id[I
  * a caller that retries the iterate must pass T_apply = null. */
 typedef int (*icp_hip_exchange_fn)(void* user, const double* local, int32_t count, double* gathered);
 int icp_hip_comm_init_host(icp_hip_ctx* ctx, int nranks, int rank, icp_hip_exchange_fn exchange, void* user);
+
+/* Abort this rank's RCCL communicator (ncclCommAbort): collectives it has enqueued that a failed
+ * peer will never join return, so the stream drains and icp_hip_destroy cannot block. For a
+ * rank whose peer failed (one process per GPU; the multi-device context does this itself). The
+ * context's iterate then fails with ICP_HIP_ERCCL until comm_init / comm_init_host is called
+ * again. No communicator: nothing to do. */
+int icp_hip_comm_abort(icp_hip_ctx* ctx);
 
 /* Build the reference octree of the target (AoS xyz, n points) and keep it in HBM. The tree is
  * built on the device (max_depth <= 21, config octree_builder AUTO) or on the host (deeper
@@ -284,7 +307,9 @@ int icp_hip_target_info(icp_hip_ctx* ctx, int64_t* n_nodes, int64_t* n_leaves, i
                         int32_t* stack_levels);
 
 /* Time (ms, HIP events on the context's stream) of the last search-kernel launch, and of the
- * whole device part of the last iterate. */
+ * whole device part of the last iterate. ICP_HIP_ENOTREADY when config.timing_stride left the
+ * last iterate untimed (the default timing_stride 0 times none: an event on a dispatch delays
+ * the next kernel). */
 int icp_hip_last_timing(icp_hip_ctx* ctx, double* nn_kernel_ms, double* iterate_device_ms);
 
 /* The same for each of the last k iterates (k <= 256, the context's timing ring), oldest first;
@@ -297,6 +322,12 @@ int icp_hip_timings(icp_hip_ctx* ctx, int k, double* nn_kernel_ms, double* itera
 int icp_hip_debug_counters(icp_hip_ctx* ctx, uint64_t out[ICP_DBG_SLOTS]);
 
 int icp_hip_synchronize(icp_hip_ctx* ctx);
+
+/* Testing hook (failure paths of the multi-rank and multi-device iterate): the next iterate of
+ * member `member` of a multi-device context (0 for a single-device one) fails with
+ * ICP_HIP_EDEVICE just before its first record exchange, i.e. after its search and before it
+ * joins the collective its peers are waiting in. where = 0 clears it. */
+int icp_hip_debug_inject_failure(icp_hip_ctx* ctx, int member, int where);
 
 const char* icp_hip_last_error(void);
 

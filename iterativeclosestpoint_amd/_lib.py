@@ -23,14 +23,17 @@ XPORT_AUTO = 0
 XPORT_RCCL = 1
 XPORT_HOST = 2
 XPORT_CALLBACK = 3
-DBG_SLOTS = 24
+# icp_hip.h error codes (IcpError.code)
+OK, EINVAL, ENOMEM, EDEVICE, ERCCL, ENOTREADY, EEXCHANGE = 0, -1, -2, -3, -4, -5, -6
+DBG_SLOTS = 32
 # icp_hip.h ICP_DBG_* slot names
 DBG_NAMES = {0: "waves", 1: "overflow_waves", 2: "not_joined", 3: "not_covered", 4: "scanned_points",
              8: "fp64_scan_waves", 9: "staged_points", 10: "scan_pairs", 11: "scan_rounds",
              12: "cache_hits", 13: "cache_stores",
              5: "walk_batches", 6: "no_guess", 7: "candidates", 14: "ball_overflow", 15: "ball_points",
              21: "start_nodes", 20: "winner_prev_waves", 22: "winner_prev", 23: "winner_lanes",
-             18: "prev_cert_waves", 19: "prev_cert_lanes", 16: "halves", 17: "reused_entries"}
+             18: "prev_cert_waves", 19: "prev_cert_lanes", 16: "halves", 17: "reused_entries",
+             24: "walk_moved", 25: "walk_loose"}
 
 _P = C.c_void_p
 _D = C.POINTER(C.c_double)
@@ -68,7 +71,7 @@ class HipConfig(C.Structure):
         ("xcd_blocks", C.c_int32), ("scan_groups", C.c_int32), ("candidate_cache", C.c_int32),
         ("candidate_margin", C.c_int32), ("certify_prev", C.c_int32), ("query_order", C.c_int32),
         ("overflow_halves", C.c_int32), ("device_loop", C.c_int32), ("timing_stride", C.c_int32),
-        ("candidate_loose", C.c_int32), ("reserved", C.c_int32 * 1),
+        ("candidate_loose", C.c_int32), ("candidate_lead", C.c_int32),
     ]
 
 
@@ -163,6 +166,8 @@ SIGNATURES = {
     "icp_hip_copy_target": (C.c_int, [_P, _P, _P, _P, _P, _P, _P]),
     "icp_hip_target_separation": (C.c_int, [_P, _P]),
     "icp_hip_synchronize": (C.c_int, [_P]),
+    "icp_hip_comm_abort": (C.c_int, [_P]),
+    "icp_hip_debug_inject_failure": (C.c_int, [_P, C.c_int, C.c_int]),
     "icp_hip_last_error": (C.c_char_p, []),
     # icp_engine.h
     "icp_params_default": (None, [C.POINTER(Params)]),
@@ -441,6 +446,14 @@ class Context:
 
     def synchronize(self):
         _check(lib().icp_hip_synchronize(self._h))
+
+    def comm_abort(self):
+        """Abort this rank's RCCL communicator (icp_hip_comm_abort)."""
+        _check(lib().icp_hip_comm_abort(self._h))
+
+    def inject_failure(self, member: int = 0, where: int = 1):
+        """Testing hook: member's next iterate fails before its first record exchange."""
+        _check(lib().icp_hip_debug_inject_failure(self._h, member, where))
 
     def debug_counters(self) -> dict:
         """The wave search's diagnostic counters of the last iterate (needs debug_counters=1)."""

@@ -144,6 +144,7 @@ void icp_hip_config_default(icp_hip_config* cfg) {
   cfg->candidate_cache = 1;
   cfg->candidate_margin = 16;
   cfg->candidate_loose = 190;
+  cfg->candidate_lead = 8;
   cfg->overflow_halves = 1;
   cfg->device_loop = 0;
   cfg->timing_stride = 0;
@@ -170,6 +171,7 @@ int icp_hip_create_ex(icp_hip_ctx** out, int device, const icp_hip_config* cfg) 
   if (conf.candidate_loose == 0) conf.candidate_loose = 190;
   if (conf.candidate_loose < 100 || conf.candidate_loose > 100000)
     return fail(ICP_HIP_EINVAL, "config: candidate_loose out of [100, 100000]");
+  if (conf.candidate_lead < 0 || conf.candidate_lead > 64) return fail(ICP_HIP_EINVAL, "config: candidate_lead out of [0, 64]");
   if (conf.overflow_halves != 0 && conf.overflow_halves != 1) return fail(ICP_HIP_EINVAL, "config: overflow_halves must be 0 or 1");
   if (conf.query_order != 0 && conf.query_order != 1) return fail(ICP_HIP_EINVAL, "config: query_order must be 0 or 1");
   if (conf.certify_prev < 0 || conf.certify_prev > 3) return fail(ICP_HIP_EINVAL, "config: certify_prev out of [0, 3]");
@@ -266,6 +268,7 @@ int icp_hip_comm_init(icp_hip_ctx* c, int nranks, int rank, const uint8_t id_byt
   // back to a world of one first: a failure below leaves no stale transport behind
   if (c->comm) (void)ncclCommDestroy(c->comm);
   c->comm = nullptr;
+  c->comm_aborted = false;
   c->xfn = nullptr;
   c->xuser = nullptr;
   c->nranks = 1;
@@ -286,10 +289,23 @@ int icp_hip_comm_init(icp_hip_ctx* c, int nranks, int rank, const uint8_t id_byt
 
 }  // extern "C"
 
+void icp_ctx_abort_comm(icp_hip_ctx* c) {
+  if (!c->comm) return;
+  (void)hipSetDevice(c->device);
+  // the collectives this communicator has enqueued return (their outputs are garbage, never read:
+  // the iterate that enqueued them has failed), so the stream drains
+  (void)ncclCommAbort(c->comm);
+  c->comm = nullptr;
+  c->comm_aborted = true;
+  (void)hipStreamSynchronize(c->stream);
+  (void)hipGetLastError();
+}
+
 int icp_ctx_attach_comm(icp_hip_ctx* c, ncclComm_t comm, int nranks, int rank) {
   HIP_TRY(hipSetDevice(c->device));
   if (c->comm) (void)ncclCommDestroy(c->comm);
   c->comm = nullptr;
+  c->comm_aborted = false;
   c->xfn = nullptr;
   c->xuser = nullptr;
   c->nranks = 1;
@@ -313,6 +329,7 @@ int icp_hip_comm_init_host(icp_hip_ctx* c, int nranks, int rank, icp_hip_exchang
   HIP_TRY(hipSetDevice(c->device));
   if (c->comm) (void)ncclCommDestroy(c->comm);
   c->comm = nullptr;
+  c->comm_aborted = false;
   c->xfn = nullptr;
   c->xuser = nullptr;
   c->nranks = 1;
@@ -581,6 +598,7 @@ static int enqueue_iterate(icp_hip_ctx* c, const double* T_apply, bool apply, in
   a.wc_gen = c->wc_gen;
   a.wc_margin = c->cfg.candidate_margin / 256.0;
   a.wc_loose = c->cfg.candidate_loose / 100.0;
+  a.wc_lead = (double)c->cfg.candidate_lead;
   if (!c->lists_zero) HIP_TRY(hipMemsetAsync(c->fb_count, 0, 8 * sizeof(unsigned int), s));
   c->lists_zero = false;
   if (c->dbg) HIP_TRY(hipMemsetAsync(c->dbg, 0, ICP_DBG_SLOTS * sizeof(unsigned long long), s));
@@ -593,6 +611,10 @@ static int enqueue_iterate(icp_hip_ctx* c, const double* T_apply, bool apply, in
   HIP_TRY(launch_nn(a, s));
   // residual moments -> mean, std, threshold (no communicator: fused into the last merge level)
   const bool multi = c->comm != nullptr || c->xfn != nullptr;
+  if (multi && c->inject_failure == 1) {  // testing hook: fail before joining the exchange
+    c->inject_failure = 0;
+    return fail(ICP_HIP_EDEVICE, "injected failure before the record exchange (icp_hip_debug_inject_failure)");
+  }
   const MomentsFinalize fin{sigma_multiplier, iter, rules == ICP_RULES_ENGINE ? 1 : 0};
   CullLaunch cl;
   cl.loop = loop;
@@ -647,6 +669,7 @@ int icp_hip_iterate(icp_hip_ctx* c, const double* T_apply, int iter, int rules, 
   if (c->group) return group_iterate(c, T_apply, iter, rules, sigma_multiplier, out);
   if (!c->nodes) return fail(ICP_HIP_ENOTREADY, "target not set");
   if (!c->x && c->n_src > 0) return fail(ICP_HIP_ENOTREADY, "source not set");
+  if (c->comm_aborted) return fail(ICP_HIP_ERCCL, "iterate: the communicator was aborted (icp_hip_comm_abort); comm_init again");
   HIP_TRY(hipSetDevice(c->device));
   hipStream_t s = c->stream;
   uint64_t seq = 0;
@@ -815,7 +838,20 @@ int icp_hip_nn(icp_hip_ctx* c, const double* q, int64_t n, int32_t* idx_out, dou
   if (c->group) return icp_hip_nn(group_member(c, 0), q, n, idx_out, dist_out);  // the replicated octree
   if (!c->nodes) return fail(ICP_HIP_ENOTREADY, "target not set");
   if (n == 0) return ICP_HIP_OK;
-  if (n > (int64_t)0x7fffffff) return fail(ICP_HIP_EINVAL, "too many queries");
+  // the wave search addresses per-query arrays by 32-bit byte offsets (nn_device.h qat): launches
+  // of fewer than 2^29 queries, so larger sets go in slices (the answers are per query)
+  constexpr int64_t kSlice = (int64_t)1 << 28;
+  if (n > kSlice) {
+    unsigned int lists[3] = {0, 0, 0};
+    for (int64_t off = 0; off < n; off += kSlice) {
+      const int64_t m = n - off < kSlice ? n - off : kSlice;
+      const int rc = icp_hip_nn(c, q + 3 * off, m, idx_out ? idx_out + off : nullptr, dist_out ? dist_out + off : nullptr);
+      if (rc != ICP_HIP_OK) return rc;
+      for (int k = 0; k < 3; k++) lists[k] += c->last_lists[k];
+    }
+    for (int k = 0; k < 3; k++) c->last_lists[k] = lists[k];
+    return ICP_HIP_OK;
+  }
   HIP_TRY(hipSetDevice(c->device));
   double *aos = nullptr, *x = nullptr, *y = nullptr, *z = nullptr, *d = nullptr, *dd = nullptr;
   int32_t *pos = nullptr, *di = nullptr;
@@ -925,7 +961,24 @@ int icp_hip_last_timing(icp_hip_ctx* c, double* nn_ms, double* it_ms) {
   if (!c) return fail(ICP_HIP_EINVAL, "null ctx");
   if (c->group) return group_timings(c, 1, nn_ms, it_ms);
   if (c->n_iterates == 0) return fail(ICP_HIP_ENOTREADY, "no iterate has run");
+  if (!c->timed[(c->n_iterates - 1) % icp_hip_ctx::kTimingRing])
+    return fail(ICP_HIP_ENOTREADY, "the last iterate was not timed (config.timing_stride)");
   return icp_hip_timings(c, 1, nn_ms, it_ms);
+}
+
+int icp_hip_comm_abort(icp_hip_ctx* c) {
+  if (!c) return fail(ICP_HIP_EINVAL, "null ctx");
+  if (c->group) return fail(ICP_HIP_EINVAL, "a multi-device context aborts its communicators itself");
+  icp_ctx_abort_comm(c);
+  return ICP_HIP_OK;
+}
+
+int icp_hip_debug_inject_failure(icp_hip_ctx* c, int member, int where) {
+  if (!c || where < 0 || where > 1) return fail(ICP_HIP_EINVAL, "bad arguments");
+  if (c->group) return group_inject_failure(c, member, where);
+  if (member != 0) return fail(ICP_HIP_EINVAL, "a single-device context has member 0 only");
+  c->inject_failure = where;
+  return ICP_HIP_OK;
 }
 
 int icp_hip_synchronize(icp_hip_ctx* c) {

@@ -81,6 +81,8 @@ struct icp_hip_ctx {
   icp::CovMoments* gc = nullptr;
   // a member of a multi-device context: set when a peer member failed (the waits give up)
   const std::atomic<int>* abort = nullptr;
+  bool comm_aborted = false;  // icp_hip_comm_abort: iterates fail until the next comm_init
+  int inject_failure = 0;     // icp_hip_debug_inject_failure: 1 = fail before the first exchange
 
   // multi-device context (icp_hip_create_multi): the member contexts and their driver threads
   // (icp_group.cpp); the single-device fields above are then unused
@@ -101,6 +103,8 @@ int icp_hip_loop_run(icp_hip_ctx* c, icp::SessionCore* core, const icp::SessionP
 // Attach a communicator created elsewhere (ncclCommInitAll of a multi-device context); the
 // context owns it from then on.
 int icp_ctx_attach_comm(icp_hip_ctx* c, ncclComm_t comm, int nranks, int rank);
+// ncclCommAbort of the context's communicator (icp_hip_comm_abort without the argument checks)
+void icp_ctx_abort_comm(icp_hip_ctx* c);
 
 // The multi-device context (icp_group.cpp): every C-ABI entry point of icp_ctx.hip dispatches here
 // when ctx->group is set.
@@ -116,4 +120,5 @@ int group_traversal_counts(icp_hip_ctx* c, double* mean_entries, double* mean_po
 int group_timings(icp_hip_ctx* c, int k, double* nn_ms, double* it_ms);
 int group_debug_counters(icp_hip_ctx* c, uint64_t out[ICP_DBG_SLOTS]);
 int group_synchronize(icp_hip_ctx* c);
+int group_inject_failure(icp_hip_ctx* c, int member, int where);
 icp_hip_ctx* group_member(icp_hip_ctx* c, int k);

@@ -110,6 +110,12 @@ struct LocalExchange {
     std::lock_guard<std::mutex> g(m);
     cv.notify_all();
   }
+  // before a job: an exchange abandoned by a failed job (some members arrived, then gave up)
+  // must not count towards the next one
+  void reset() {
+    std::lock_guard<std::mutex> g(m);
+    arrived = 0;
+  }
 };
 
 struct ExchangeSlot {
@@ -131,7 +137,10 @@ struct DeviceGroup {
   std::unique_ptr<LocalExchange> lx;
   std::vector<ExchangeSlot> slots;
   std::vector<std::unique_ptr<Driver>> drivers;
-  std::atomic<int> abort{0};
+  std::atomic<int> abort{0};  // a member of the running job failed (peers stop waiting)
+  // an iterate failed over RCCL: the communicators were aborted, only destroy is left
+  bool dead = false;
+  std::string dead_why;
   // the source: caller index of group slot k, and member m's slots [lo[m], lo[m + 1])
   std::vector<int32_t> order;
   std::vector<int64_t> lo;
@@ -149,7 +158,13 @@ int fail(int code, const std::string& msg) {
 // (the message is thread-local to the driver that saw it) come back to the caller. A failing member
 // raises the group's abort flag, so peers waiting in an exchange or for a record give up.
 int for_members(DeviceGroup* g, const std::function<int(int, icp_hip_ctx*)>& f) {
+  if (g->dead)
+    return fail(ICP_HIP_EDEVICE, "multi-device context unusable after a failed RCCL iterate (" + g->dead_why +
+                                     "); destroy it and create a new one");
   const int n = (int)g->members.size();
+  // a new job starts clean: the flag and the host exchange's count of the previous failed job
+  g->abort.store(0);
+  if (g->lx) g->lx->reset();
   std::vector<int> rc((size_t)n, ICP_HIP_OK);
   std::vector<std::string> msg((size_t)n);
   for (int k = 0; k < n; k++) {
@@ -283,6 +298,7 @@ int group_set_source(icp_hip_ctx* c, const double* xyz, int64_t n) {
   DeviceGroup* g = c->group;
   const int w = (int)g->members.size();
   if (n < w) return fail(ICP_HIP_EINVAL, "set_source: a multi-device context needs at least one point per device");
+  if (n > (int64_t)0x7fffffff) return fail(ICP_HIP_EINVAL, "set_source: 2^31 points or more (int32 query order)");
   // spatially compact shards: contiguous ranges of the kd order (icp_source_shard_order's order),
   // built on the first device (or on the host: config query_order = 1, or no device memory)
   g->order.assign((size_t)n, 0);
@@ -318,9 +334,27 @@ int group_set_source(icp_hip_ctx* c, const double* xyz, int64_t n) {
 int group_iterate(icp_hip_ctx* c, const double* T_apply, int iter, int rules, double sigma, icp_iter_stats* out) {
   DeviceGroup* g = c->group;
   const int w = (int)g->members.size();
+  if (!g->dead) {  // usage errors before any member runs leave the group usable
+    for (icp_hip_ctx* m : g->members) {
+      if (!m->nodes) return fail(ICP_HIP_ENOTREADY, "target not set");
+      if (!m->x && m->n_src > 0) return fail(ICP_HIP_ENOTREADY, "source not set");
+    }
+  }
   std::vector<icp_iter_stats> st((size_t)w);
   const int rc = for_members(g, [&](int k, icp_hip_ctx* m) { return icp_hip_iterate(m, T_apply, iter, rules, sigma, &st[k]); });
-  if (rc != ICP_HIP_OK) return rc;
+  if (rc != ICP_HIP_OK) {
+    if (g->transport == ICP_XPORT_RCCL && !g->dead) {
+      // A member that failed before joining a collective leaves its peers' streams holding one
+      // that never completes: abort every communicator (the pending collectives return, the
+      // streams drain, destroy cannot block). The group cannot exchange again.
+      const std::string why = icp_hip_last_error();
+      for (icp_hip_ctx* m : g->members) icp_ctx_abort_comm(m);
+      g->dead = true;
+      g->dead_why = why;
+      return fail(rc, why);
+    }
+    return rc;
+  }
   // the statistics are merged in rank order on every device: identical on all members
   for (int k = 1; k < w; k++)
     if (st[k].valid != st[0].valid || std::memcmp(&st[k].mean, &st[0].mean, sizeof(double)) != 0 ||
@@ -418,6 +452,13 @@ int group_synchronize(icp_hip_ctx* c) {
     const int rc = icp_hip_synchronize(m);
     if (rc != ICP_HIP_OK) return rc;
   }
+  return ICP_HIP_OK;
+}
+
+int group_inject_failure(icp_hip_ctx* c, int member, int where) {
+  DeviceGroup* g = c->group;
+  if (member < 0 || member >= (int)g->members.size()) return fail(ICP_HIP_EINVAL, "inject_failure: no such member");
+  g->members[member]->inject_failure = where;
   return ICP_HIP_OK;
 }
 

@@ -88,6 +88,7 @@ struct NNLaunch {
   uint32_t wc_gen;          // records of this generation are valid
   double wc_margin;         // a walk collects the leaves of B enlarged by this x B's half-extent
   double wc_loose;          // a record is reused only while vol(B+) <= this x vol(B)
+  double wc_lead;           // a stored B+ leads the wave's motion by this many iterates' displacement
   int certify_prev;         // previous-match certificate mode (icp_hip_config.certify_prev)
 };
 

@@ -543,6 +543,10 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
       reuse = (uint32_t)(cg >> 32) == a.wc_gen && blx >= hlx && bly >= hly && blz >= hlz && bhx <= hhx &&
               bhy <= hhy && bhz <= hhz &&
               (hhx - hlx) * (hhy - hly) * (hhz - hlz) <= a.wc_loose * ((bhx - blx) * (bhy - bly) * (bhz - blz));
+      if (kDbg && a.dbg && lane == 0 && !reuse && (uint32_t)(cg >> 32) == a.wc_gen) {
+        const bool inside = blx >= hlx && bly >= hly && blz >= hlz && bhx <= hhx && bhy <= hhy && bhz <= hhz;
+        atomicAdd(&a.dbg[inside ? 25 : 24], 1ull);
+      }
       if (reuse) {
         nleaf = (int)(uint32_t)cg;
         flx = hlx;
@@ -565,23 +569,47 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
       // re-walks anyway) the wave walks B itself and stores nothing.
       const bool keep = wb && a.have_prev;
       const double m = keep ? a.wc_margin * 0.5 * dmax_(dmax_(bhx - blx, bhy - bly), bhz - blz) : 0.0;
-      wlx = uniform_d(blx - m);
-      wly = uniform_d(bly - m);
-      wlz = uniform_d(blz - m);
-      whx = uniform_d(bhx + m);
-      why = uniform_d(bhy + m);
-      whz = uniform_d(bhz + m);
+      // The lead: the queries of a wave keep moving the same way for many iterates (ICP's
+      // increments change slowly), so the stored B+ also covers where B will be after wc_lead
+      // more iterates of this iterate's motion (the displacement of B's centre by the applied
+      // transform), on the side it moves to. Any box is exact: this only sets how long the
+      // record lasts against how many entries a reusing wave streams.
+      double dlx = 0.0, dly = 0.0, dlz = 0.0, dhx = 0.0, dhy = 0.0, dhz = 0.0;
+      if (APPLY && keep && a.wc_lead > 0.0) {
+        const double* T = a.loop ? a.loop->core.T : a.T;
+        const double cx = (blx + bhx) * 0.5, cy = (bly + bhy) * 0.5, cz = (blz + bhz) * 0.5;
+        const double ex = (((T[0] * cx + T[1] * cy) + T[2] * cz) + T[3]) - cx;
+        const double ey = (((T[4] * cx + T[5] * cy) + T[6] * cz) + T[7]) - cy;
+        const double ez = (((T[8] * cx + T[9] * cy) + T[10] * cz) + T[11]) - cz;
+        // finite and at most B's largest extent per iterate (a wild increment leads nowhere)
+        const double cap = 2.0 * dmax_(dmax_(bhx - blx, bhy - bly), bhz - blz);
+        auto lead = [&](double e) { return (e == e && __builtin_fabs(e) <= cap) ? a.wc_lead * e : 0.0; };
+        const double lx = lead(ex), ly = lead(ey), lz = lead(ez);
+        dlx = lx < 0.0 ? -lx : 0.0;
+        dhx = lx > 0.0 ? lx : 0.0;
+        dly = ly < 0.0 ? -ly : 0.0;
+        dhy = ly > 0.0 ? ly : 0.0;
+        dlz = lz < 0.0 ? -lz : 0.0;
+        dhz = lz > 0.0 ? lz : 0.0;
+      }
+      wlx = uniform_d(blx - (m + dlx));
+      wly = uniform_d(bly - (m + dly));
+      wlz = uniform_d(blz - (m + dlz));
+      whx = uniform_d(bhx + (m + dhx));
+      why = uniform_d(bhy + (m + dhy));
+      whz = uniform_d(bhz + (m + dhz));
       walk(wlx, wly, wlz, whx, why, whz);
-      if (ICP_SHRINK_RETRY && overflow && keep) {
-        // B+ holds too many points: walk again with a quarter of the margin and store that list
-        // (an overflowing wave that stored nothing would overflow again at every iterate)
+      if (overflow && keep) {
+        // B+ holds too many points: walk again with a quarter of the margin and the lead, and
+        // store that list (an overflowing wave that stored nothing would overflow again at every
+        // iterate)
         const double m4 = 0.25 * m;
-        wlx = uniform_d(blx - m4);
-        wly = uniform_d(bly - m4);
-        wlz = uniform_d(blz - m4);
-        whx = uniform_d(bhx + m4);
-        why = uniform_d(bhy + m4);
-        whz = uniform_d(bhz + m4);
+        wlx = uniform_d(blx - (m4 + 0.25 * dlx));
+        wly = uniform_d(bly - (m4 + 0.25 * dly));
+        wlz = uniform_d(blz - (m4 + 0.25 * dlz));
+        whx = uniform_d(bhx + (m4 + 0.25 * dhx));
+        why = uniform_d(bhy + (m4 + 0.25 * dhy));
+        whz = uniform_d(bhz + (m4 + 0.25 * dhz));
         walk(wlx, wly, wlz, whx, why, whz);
       }
       wstore = keep && !overflow;

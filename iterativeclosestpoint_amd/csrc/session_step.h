@@ -84,7 +84,7 @@ ICP_HD int32_t session_core_step(SessionCore& s, const SessionParams& p, double 
   }
   if (!stop) {
     s.prev = rmse;
-    if ((int32_t)valid < 3) {
+    if ((int64_t)valid < 3) {
       s.status = ICP_STATUS_TOO_FEW;
       if (!p.cli) s.too_few = 1;
       out = kStepTooFew;

@@ -103,6 +103,79 @@ def test_group_argument_errors(icp, pair):
             ctx.comm_init_host(2, 0, lambda local: np.stack([local, local]))
 
 
+def test_group_member_failure_host_gather(icp, pair, plain):
+    """A member failing before the record exchange (icp_hip_debug_inject_failure) fails the iterate
+    with its own error in bounded time (the peers waiting in the host gather give up), harmless
+    errors do not poison the group, and the same group then runs a clean registration that equals
+    the plain run (the abort flag and the exchange count are reset per job)."""
+    import time
+    tgt, src = pair
+    with icp.Context(devices=[0, 0, 0]) as ctx:
+        ctx.set_target(tgt, 10, 20, icp.RULES_ENGINE)
+        ctx.set_source(src)
+        with pytest.raises(icp.IcpError) as e:
+            ctx.get_correspondences()  # no iterate yet: a harmless error
+        assert e.value.code == icp.ENOTREADY
+        ctx.inject_failure(member=1)
+        t0 = time.perf_counter()
+        with pytest.raises(icp.IcpError) as e:
+            ctx.iterate(None, 0, icp.RULES_ENGINE, 3.0)
+        assert time.perf_counter() - t0 < 30.0
+        assert e.value.code == icp.EDEVICE and "injected" in str(e.value)
+        recs, corr, moved = _run(icp, ctx, tgt, src)
+    p_recs, _, p_moved = plain
+    for (v, rmse, *_r), (pv, prmse, *_p) in zip(recs, p_recs):
+        assert v == pv
+        np.testing.assert_allclose(rmse, prmse, rtol=1e-12)
+    np.testing.assert_allclose(moved, p_moved, rtol=0, atol=1e-9)
+
+
+def test_group_member_failure_rccl_aborts(icp, pair):
+    """Over RCCL a failed iterate aborts every member's communicator (ncclCommAbort) and leaves the
+    group dead: later calls fail with EDEVICE instead of hanging on a collective a failed peer never
+    joined, and destroy returns. One device here (ncclCommInitAll of one rank): the same code path
+    as N GPUs."""
+    import time
+    tgt, src = pair
+    ctx = icp.Context(devices=[0], transport=icp.XPORT_RCCL)
+    try:
+        ctx.set_target(tgt, 10, 20, icp.RULES_ENGINE)
+        ctx.set_source(src)
+        ctx.iterate(None, 0, icp.RULES_ENGINE, 3.0)  # a good iterate first
+        ctx.inject_failure(member=0)
+        t0 = time.perf_counter()
+        with pytest.raises(icp.IcpError) as e:
+            ctx.iterate(None, 1, icp.RULES_ENGINE, 3.0)
+        assert e.value.code == icp.EDEVICE
+        with pytest.raises(icp.IcpError) as e:
+            ctx.iterate(None, 2, icp.RULES_ENGINE, 3.0)
+        assert e.value.code == icp.EDEVICE and "destroy" in str(e.value)
+        assert time.perf_counter() - t0 < 30.0
+    finally:
+        t0 = time.perf_counter()
+        ctx.close()
+        assert time.perf_counter() - t0 < 30.0
+
+
+def test_comm_abort_single_rank(icp, pair):
+    """icp_hip_comm_abort on a one-rank RCCL communicator: iterates fail with ERCCL until the next
+    comm_init, which restores the bit-identical multi-rank path."""
+    tgt, src = pair
+    with icp.Context(0) as ctx:
+        ctx.set_target(tgt, 10, 20, icp.RULES_ENGINE)
+        ctx.set_source(src)
+        ctx.comm_init(1, 0, icp.Context.unique_id())
+        a = ctx.iterate(None, 0, icp.RULES_ENGINE, 3.0)
+        ctx.comm_abort()
+        with pytest.raises(icp.IcpError) as e:
+            ctx.iterate(None, 1, icp.RULES_ENGINE, 3.0)
+        assert e.value.code == icp.ERCCL
+        ctx.comm_init(1, 0, icp.Context.unique_id())
+        ctx.set_source(src)
+        b = ctx.iterate(None, 0, icp.RULES_ENGINE, 3.0)
+    assert (a.valid, a.rmse) == (b.valid, b.rmse)
+
+
 def test_engine_and_cli_with_device_lists(icp, pair):
     tgt, src = pair
     p = icp.params_default(max_iterations=20, tolerance=1e-9)
