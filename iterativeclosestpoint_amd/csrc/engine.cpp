@@ -19,7 +19,7 @@
 #include "../../include/icp_engine.h"
 #include "icp_ctx_internal.h"
 #include "session_step.h"
-#include "svd3.h"
+#include "svd3_impl.h"  // the 3x3 Jacobi SVD and best fit (host + device, Eigen JacobiSVD order)
 
 namespace {
 
@@ -60,12 +60,12 @@ void icp_params_default(icp_params* p) {
   p->flags = 0;
 }
 
-void icp_jacobi_svd3(const double H[9], double U[9], double S[3], double V[9]) { icp::jacobi_svd3(H, U, S, V); }
+void icp_jacobi_svd3(const double H[9], double U[9], double S[3], double V[9]) { icp::svd::jacobi_svd3(H, U, S, V); }
 
-void icp_mat4_mul(const double A[16], const double B[16], double C[16]) { icp::mat4_mul(A, B, C); }
+void icp_mat4_mul(const double A[16], const double B[16], double C[16]) { icp::svd::mat4_mul(A, B, C); }
 
 void icp_best_fit_from_stats(const icp_iter_stats* st, double T[16]) {
-  icp::best_fit_from_moments(st->centroid_src, st->centroid_tgt, st->H, T);
+  icp::svd::best_fit_from_moments(st->centroid_src, st->centroid_tgt, st->H, T);
 }
 
 void icp_best_fit_transform(const double* a, const double* b, int64_t n, double T[16]) {
@@ -86,7 +86,7 @@ void icp_best_fit_transform(const double* a, const double* b, int64_t n, double 
   for (int64_t i = 0; i < n; i++)
     for (int r = 0; r < 3; r++)
       for (int c = 0; c < 3; c++) C[3 * r + c] += (a[3 * i + r] - ma[r]) * (b[3 * i + c] - mb[c]);
-  icp::best_fit_from_moments(ma, mb, C, T);
+  icp::svd::best_fit_from_moments(ma, mb, C, T);
 }
 
 }  // extern "C"

@@ -29,35 +29,6 @@
 #ifndef ICP_PHASE_CLOCKS
 #define ICP_PHASE_CLOCKS 0
 #endif
-#ifndef ICP_SHRINK_RETRY
-#define ICP_SHRINK_RETRY 1
-#endif
-// Staging layout of the fp32 scan for NG <= 2: each scan group's pairs contiguous (1: its
-// scattered stores meet a bank at most twice, but the layout costs two more spilled registers:
-// search 0.487-0.489 ms vs 0.478-0.481 at 10M, same box) or the groups interleaved (0, default)
-#ifndef ICP_STAGE_CONTIG
-#define ICP_STAGE_CONTIG 0
-#endif
-#ifndef ICP_SCAN_UNROLL
-#define ICP_SCAN_UNROLL 1
-#endif
-// Timing: the search's end as its own dispatch's stop event (1) or the next kernel's start (0)
-#ifndef ICP_SEARCH_STOP_EVENT
-#define ICP_SEARCH_STOP_EVENT 1
-#endif
-// The first iterate's guess: the nearest point of every leaf child of the descent leaf's parent
-// (1) or of the descent leaf alone (0)
-#ifndef ICP_DESCENT_SIBLINGS
-#define ICP_DESCENT_SIBLINGS 1
-#endif
-#ifndef ICP_SKIP_PREV_GATHER
-#define ICP_SKIP_PREV_GATHER 0
-#endif
-// Diagnostic build only (-DICP_WINNER_COUNTS=1): debug slots 20, 22, 23 count how often the fp32
-// winner is the previous match (its registers would otherwise cost the product build a spill).
-#ifndef ICP_WINNER_COUNTS
-#define ICP_WINNER_COUNTS 0
-#endif
 constexpr bool kDbgCounts = !ICP_PHASE_CLOCKS;  // the clock build counts nothing (no atomics)
 #if ICP_PHASE_CLOCKS
 #define PCLK(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
@@ -275,7 +246,7 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
         scan_leaf(topo);
         // (in the instances without a transform: a session's first iterate; the steady-state
         // instances keep their registers for the scan)
-        if (ICP_DESCENT_SIBLINGS && !APPLY && pfirst >= 0) {
+        if (!APPLY && pfirst >= 0) {
           // then the points of the parent's other leaf children whose box is nearer than the
           // best so far (~3 points per leaf: the reached leaf alone bounds the nearest distance
           // loosely, and the first iterate's boxes, overflows and ball searches grow with it)
@@ -702,15 +673,12 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
         gh[g][2] = uni((ghi[g][2] + doz) + mg);
       }
       constexpr int S = 64 / NG;  // lanes of a group = points of a group's segment per round
-      constexpr int S_ = S;
       const int gq = lane / S;    // this lane's group
       // staging area: NG segments of S points, in pairs [x0 x1 y0 y1 z0 z1 w0 w1] (32 B) so that
       // one packed fp32 instruction (v_pk_add/mul/fma_f32) evaluates an axis of two points.
-      // Pair k of group g: NG <= 2, at g S/2 + k (each group's pairs contiguous: a group's scattered
-      // stores, 32 lanes x 4 B, meet each bank at most twice, which ds_write_b32 absorbs; with the
-      // groups interleaved they met it 4 times); NG = 4, at k NG + g (the b128 read lane groups
-      // mix two scan groups, whose concurrent broadcast reads then fall on distinct banks)
-      auto blk = [](int k, int g) { return (NG == 4 || !ICP_STAGE_CONTIG) ? k * NG + g : g * (S_ / 2) + k; };
+      // Pair k of group g at k NG + g: the groups interleaved (each group's pairs contiguous costs
+      // two more spilled registers)
+      auto blk = [](int k, int g) { return k * NG + g; };
       float* stage32 = reinterpret_cast<float*>(wl);
       // Selection keys: the fp32 squared distance with its low 6 bits replaced by the point's slot
       // in the segment (v_bfi), so that the two smallest are kept by two med3 per point and the
@@ -743,7 +711,7 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
         sel(sq.y, (uint32_t)__builtin_amdgcn_readfirstlane((int)(sl + 1u)));  // a scalar operand
       };
       const v4i* st4 = reinterpret_cast<const v4i*>(stage32) + 2 * blk(0, gq);  // this group's pair 0
-      constexpr int kStep = (NG == 4 || !ICP_STAGE_CONTIG) ? 2 * NG : 2;        // v4i per pair step
+      constexpr int kStep = 2 * NG;                                             // v4i per pair step
       // One chunk of 64 candidates (lane = candidate base + lane; offsets vx, vy, vz, id bits vw):
       // group membership, rank among the group's points of the chunk, and (first round) the store
       // into the group's segment; `next` issues the following chunk's loads once this one is
@@ -809,20 +777,8 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
             atomicAdd(&a.dbg[10], (unsigned long long)mp);
             atomicAdd(&a.dbg[11], 1ull);
           }
-#if ICP_SCAN_UNROLL == 2
-          {
-            int k = 0;
-#pragma unroll 1
-            for (; k + 1 < mp; k += 2) {
-              eval2(st4[kStep * k], st4[kStep * k + 1], 2u * k);
-              eval2(st4[kStep * k + kStep], st4[kStep * k + kStep + 1], 2u * k + 2u);
-            }
-            if (k < mp) eval2(st4[kStep * k], st4[kStep * k + 1], 2u * k);
-          }
-#else
 #pragma unroll 1
           for (int k = 0; k < mp; k++) eval2(st4[kStep * k], st4[kStep * k + 1], 2u * k);
-#endif
           // the winner of this round, if it improved the lane's best: its index from its slot
           if (k1 != k1_in) {
             const uint32_t sl = __float_as_uint(k1) & 63u;
@@ -876,23 +832,10 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
       const float s2 = __uint_as_float(__float_as_uint(k2) & ~63u);  // <= the second-smallest value
       // fp64 distance of the fp32 winner, exactly as the leaf scan computes it (octree.cpp:139-144)
       double b64 = __builtin_inf();
-      if (ICP_SKIP_PREV_GATHER && join && p1 >= 0 && p1 == prev_pos) {
-        // the winner is the previous match: the guess evaluated exactly this expression on the
-        // same operands (moved query, same target record), so u is its fl(d2) bit for bit
-        b64 = u;
-      } else if (join && p1 >= 0) {
+      if (join && p1 >= 0) {
         const TgtPt* p = a.pts + p1;
         const double dx = p->x - qx, dy = p->y - qy, dz = p->z - qz;
         b64 = dx * dx + dy * dy + dz * dz;
-      }
-      if (ICP_WINNER_COUNTS && a.dbg) {
-        const unsigned long long same = __ballot(join && p1 >= 0 && p1 == prev_pos);
-        const unsigned long long won = __ballot(join && p1 >= 0);
-        if (lane == 0) {
-          atomicAdd(&a.dbg[22], (unsigned long long)__popcll(same));
-          atomicAdd(&a.dbg[23], (unsigned long long)__popcll(won));
-          if (won != 0 && (won & ~same) == 0) atomicAdd(&a.dbg[20], 1ull);
-        }
       }
       const double lb2 = scan32_lower_bound(s2, ext * (1.0 + 0x1p-19));
       // Decided lanes: nothing scanned; every point beyond the guess (the fp32 winner and the
@@ -1441,17 +1384,9 @@ hipError_t launch_nn(const NNLaunch& a, hipStream_t s) {
   // kernels). An event on a dispatch delays the next kernel by ~3-5 us (its start event carried
   // by the next kernel's dispatch instead measured no better), so the context times only every
   // config.timing_stride-th iterate (null events: plain launches).
-#if ICP_SEARCH_STOP_EVENT
-  hipEvent_t next_start = nullptr;
   auto wave = [&](auto kern) {
     hipExtLaunchKernelGGL(kern, dim3(wgrid), dim3(256), (uint32_t)wshm, s, a.ev_start, a.ev_fast_done, 0u, a);
   };
-#else
-  hipEvent_t next_start = a.ev_fast_done;
-  auto wave = [&](auto kern) {
-    hipExtLaunchKernelGGL(kern, dim3(wgrid), dim3(256), (uint32_t)wshm, s, a.ev_start, nullptr, 0u, a);
-  };
-#endif
   // the previous-match certificate only where it can apply (an iterate after a search)
   const bool cert = a.certify_prev != 0 && a.have_prev;
   // instances: transform, scan groups, certificate, debug counters
@@ -1483,7 +1418,7 @@ hipError_t launch_nn(const NNLaunch& a, hipStream_t s) {
     const int64_t hb = (halves + 3) / 4;
     const unsigned hgrid = (unsigned)(hb < 2048 ? hb : 2048);  // about one resident block per slot
     auto half = [&](auto kern) {
-      hipExtLaunchKernelGGL(kern, dim3(hgrid), dim3(256), (uint32_t)wshm, s, next_start, nullptr, 0u, h);
+      hipExtLaunchKernelGGL(kern, dim3(hgrid), dim3(256), (uint32_t)wshm, s, nullptr, nullptr, 0u, h);
     };
     switch (a.scan_groups + (dbg ? 8 : 0)) {
       case 1: half(k_nn_half<1, false>); break;
@@ -1494,7 +1429,6 @@ hipError_t launch_nn(const NNLaunch& a, hipStream_t s) {
       case 12: half(k_nn_half<4, true>); break;
       default: return hipErrorInvalidValue;
     }
-    next_start = nullptr;
   }
   // the follow-up lists are short (the ball list ~0.1 % of the queries, the exact list usually
   // empty): one launch of 64-thread blocks, grid-stride over them; LDS for the group stacks and
@@ -1504,7 +1438,7 @@ hipError_t launch_nn(const NNLaunch& a, hipStream_t s) {
   if (bshm < (size_t)kBallLdsBytes) bshm = kBallLdsBytes;
   static_assert(kBallGPoints * 4 >= 64 * 8, "a group's DFS stack (stride 1) holds >= 64 levels");
   if (levels > kBallGPoints * 4 / 8) return hipErrorInvalidValue;
-  hipExtLaunchKernelGGL(k_nn_ball, dim3((unsigned)(bq < 8192 ? bq : 8192)), dim3(64), (uint32_t)bshm, s, next_start,
+  hipExtLaunchKernelGGL(k_nn_ball, dim3((unsigned)(bq < 8192 ? bq : 8192)), dim3(64), (uint32_t)bshm, s, nullptr,
                         nullptr, 0u, a);
   return hipGetLastError();
 }

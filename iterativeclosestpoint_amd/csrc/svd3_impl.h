@@ -1,5 +1,7 @@
-// svd3_impl.h — the 3x3 two-sided Jacobi SVD, rigid best fit and 4x4 product of svd3.h as
-// host + device functions: the host engine (svd3.cpp) and the device-resident loop
+// svd3_impl.h — the 3x3 two-sided Jacobi SVD (the algorithm of Eigen 3.3.4's JacobiSVD that the
+// reference calls at icpengine.cpp:93 / icp_registration.cpp:418), the rigid best fit built on it
+// (icpengine.cpp:76-115, icp_registration.cpp:389-440) and the 4x4 product, as host + device
+// functions: the host engine (engine.cpp) and the device-resident loop
 // (reduce_kernels.hip, the publishing kernel) run the same operations in the same order, so with
 // IEEE fp64 (+, -, *, /, sqrt correctly rounded on both; no contraction: -ffp-contract=off) they
 // give the same bits (tests/test_gpu_parity.py::test_device_loop_*).

@@ -184,9 +184,8 @@ def las_and_report():
     """(f1) LAS 1.2 writer/reader and the transformation report of the reference CLI.
 
     saveResultAsLAS / readLASFile / saveTransformation (icp_registration.cpp:625-815, :248-378),
-    run by the compiled reference. The core LASIO (core/lasio.cpp) includes Qt headers via
-    pointcloud.h and is unbuildable here: its reader shares this arithmetic, its writer is
-    restated only (tests/test_las.py says so)."""
+    run by the compiled reference CLI. The core LASIO (core/lasio.cpp, built against the image's
+    Qt 5.9.7 by oracle/Makefile's refqt target) has fixtures of its own: core_las() below."""
     import tempfile
     rng = np.random.default_rng(77)
     n = 12345  # > one 10000-record batch, ragged tail

@@ -2,7 +2,7 @@
 # Build the working tree's library as iterativeclosestpoint_amd/libicp_hip_<tag>.so (same-box A/B of
 # uncommitted variants and diagnostic builds: ICP_HIP_LIB selects it). Runs here, not on the GPU box.
 # usage: bash tools/build_variant.sh TAG ["-DDEFINE=1 ..."]
-#   e.g. build_variant.sh clk "-DICP_PHASE_CLOCKS=1"; build_variant.sh wc "-DICP_WINNER_COUNTS=1"
+#   e.g. build_variant.sh clk "-DICP_PHASE_CLOCKS=1"
 set -eu
 TAG=$1
 EXTRA=${2:-}
