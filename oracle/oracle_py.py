@@ -55,6 +55,10 @@ def build(ref: bool = True) -> None:
         subprocess.run(["make", "-C", str(ORACLE_DIR), "ref"], check=True, capture_output=True)
     if ref and REF_CORE_SRC.exists() and QT_MOC.exists():
         subprocess.run(["make", "-C", str(ORACLE_DIR), "refqt"], check=True, capture_output=True)
+        # the reference's ICPEngine class on libicp_hip.so (integration/icpengine_hip.cpp): needs the
+        # product library, which __graft_entry__.build() compiles first
+        if (ORACLE_DIR.parent / "iterativeclosestpoint_amd" / "libicp_hip.so").exists():
+            subprocess.run(["make", "-C", str(ORACLE_DIR), "refadapter"], check=True, capture_output=True)
 
 
 _O = None
