@@ -34,7 +34,8 @@ typedef struct icp_las_header {
  * (core rules) or bad point count (CLI rules). */
 int icp_las_read_header(const char* path, int rules, icp_las_header* hdr);
 
-/* Points (AoS xyz). xyz_out must hold min(num_points, max_points) points (max_points 0 = all).
+/* Points (AoS xyz). xyz_out must hold min(num_points, max_points) points (max_points 0 = all;
+ * with CLI rules, whose reader has no limit, max_points only bounds the output buffer).
  * Returns the number of points read (>= 0) or a negative error as above. */
 int64_t icp_las_read(const char* path, int rules, int64_t max_points, double* xyz_out, icp_las_header* hdr);
 

@@ -64,7 +64,10 @@ int64_t icp_las_read(const char* path, int rules, int64_t max_points, double* xy
   f.seekg(H->offset_to_points, std::ios::beg);
   if (!f) return -1;
   int64_t n = H->num_points;
-  if (rules == ICP_LAS_CORE && max_points > 0 && max_points < n) n = max_points;  // lasio.cpp:60-63
+  // lasio.cpp:60-63 (core rules). The CLI reader has no limit (icp_registration.cpp:286-366), but
+  // max_points is also the caller's buffer capacity (icp_las.h): never read past it (found by the
+  // ASan build, tests/test_sanitize.py)
+  if (max_points > 0 && max_points < n) n = max_points;
   // Batches of 10000 records (lasio.cpp:70-103 / :326-366). A short read at end of file still
   // parses the whole batch from the (zero-initialised, then reused) buffer, as the reference.
   const int kBatch = 10000;
