@@ -204,6 +204,7 @@ int icp_hip_create_ex(icp_hip_ctx** out, int device, const icp_hip_config* cfg) 
           hipSuccess ||
       hipHostGetDevicePointer(reinterpret_cast<void**>(&c->h_it_dev), c->h_it, 0) != hipSuccess ||
       dalloc(&c->counters, 2) != hipSuccess || dalloc(&c->fb_count, 8) != hipSuccess || dalloc(&c->loopd, 1) != hipSuccess ||
+      dalloc(&c->tickets, (size_t)ticket_words()) != hipSuccess ||
       hipHostMalloc(reinterpret_cast<void**>(&c->h_loop), sizeof(LoopDev)) != hipSuccess ||
       hipHostMalloc(reinterpret_cast<void**>(&c->h_ring), icp_hip_ctx::kLoopRing * sizeof(LoopRec),
                     hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
@@ -214,6 +215,7 @@ int icp_hip_create_ex(icp_hip_ctx** out, int device, const icp_hip_config* cfg) 
   }
   (void)hipMemset(c->it, 0, sizeof(IterDev));
   (void)hipMemset(c->fb_count, 0, 8 * sizeof(unsigned int));
+  (void)hipMemset(c->tickets, 0, (size_t)ticket_words() * sizeof(unsigned int));
   if (c->dbg) (void)hipMemset(c->dbg, 0, ICP_DBG_SLOTS * sizeof(unsigned long long));
   std::memset(c->h_it, 0, sizeof(IterDev));
   c->lists_zero = true;
@@ -235,6 +237,7 @@ void icp_hip_destroy(icp_hip_ctx* c) {
   dfree(c->it);
   dfree(c->counters);
   dfree(c->fb_count);
+  dfree(c->tickets);
   dfree(c->dbg);
   dfree(c->gm);
   dfree(c->gc);
@@ -626,15 +629,14 @@ static int enqueue_iterate(icp_hip_ctx* c, const double* T_apply, bool apply, in
   cl.it = c->it;
   cl.part = c->cparts;
   cl.n = c->n_src;
-  HIP_TRY(launch_moments(c->dist, c->n_src, c->mparts, loop, s));
-  HIP_TRY(launch_merge_moments(c->mparts, c->nb_mom, c->dist, c->n_src, c->it, multi ? nullptr : &fin, cl, s));
+  HIP_TRY(launch_moments_tail(c->dist, c->n_src, c->mparts, loop, c->tickets, c->it, multi ? nullptr : &fin, cl, s));
   if (multi) {
     const int rc = all_gather_record(c, reinterpret_cast<const double*>(&c->it->m_local),
                                      reinterpret_cast<double*>(c->gm), (int)(sizeof(Moments) / sizeof(double)), s);
     if (rc != ICP_HIP_OK) return rc;
     HIP_TRY(launch_finalize_moments(c->gm, c->nranks, c->it, fin, cl, s));
   }
-  HIP_TRY(launch_cull_cov(cl, s));
+
   // covariance moments -> RMSE; the finished record is stored into pinned host memory (host
   // loop) or steps the device session (device loop)
   uint64_t seq = 0;
@@ -647,7 +649,7 @@ static int enqueue_iterate(icp_hip_ctx* c, const double* T_apply, bool apply, in
     pub.host = c->h_it_dev;
     pub.seq = (double)seq;
   }
-  HIP_TRY(launch_merge_cov(c->cparts, c->nb_cull, cl, c->it, multi ? nullptr : &pub, s));
+  HIP_TRY(launch_cull_tail(cl, c->tickets + ticket_words() / 2, multi ? nullptr : &pub, s));
   if (multi) {
     const int rc = all_gather_record(c, reinterpret_cast<const double*>(&c->it->c_local),
                                      reinterpret_cast<double*>(c->gc), (int)(sizeof(CovMoments) / sizeof(double)), s);

@@ -47,6 +47,8 @@ struct icp_hip_ctx {
   uint32_t wc_gen = 1;                   // bumped by set_target / set_source (records of older
                                          // generations are never reused)
   unsigned int* fb_count = nullptr;
+  unsigned int* tickets = nullptr;  // "last block done" counters of the moments and cull launches
+                                    // (zero between launches: the last block resets its own)
   unsigned long long* dbg = nullptr;
   unsigned int last_lists[3] = {0, 0, 0};  // exact / ball / per-lane list sizes of the last search
   icp::Moments* mparts = nullptr;

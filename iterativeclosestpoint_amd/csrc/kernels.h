@@ -112,7 +112,6 @@ struct CullLaunch {
 
 // Residual moments of the settled queries in fixed parts (deterministic), then the merges.
 int64_t moments_num_parts(int64_t n);
-hipError_t launch_moments(const double* dist, int64_t n, Moments* part, const LoopDev* loop, hipStream_t s);
 // Partial buffers need merge_scratch_entries(nparts) entries of fold scratch behind the partials.
 int64_t merge_scratch_entries(int64_t nparts);
 
@@ -121,10 +120,14 @@ struct MomentsFinalize {
   int iter;
   int engine_rules;
 };
-// Merge the rank's partials into it->m_local; with fin (no communicator) also mean/std/threshold
-// and the cull's pair shift (it->cshift, from cl's first 64 queries).
-hipError_t launch_merge_moments(const Moments* part, int64_t nparts, const double* dist, int64_t nq, IterDev* it,
-                                const MomentsFinalize* fin, const CullLaunch& cl, hipStream_t s);
+// Residual moments of the rank's queries (part sums) and their last merge level into it->m_local;
+// with fin (no communicator) also mean/std/threshold and the cull's pair shift (it->cshift, from
+// cl's first 64 queries). With a ticket counter (zero between launches) and at most 4096 parts
+// the last block of the moments launch runs the last level itself (one launch instead of two).
+// uints of the two "last block done" counters (moments, cull), zero-initialised once
+int ticket_words();
+hipError_t launch_moments_tail(const double* dist, int64_t n, Moments* part, const LoopDev* loop, unsigned* ticket,
+                               IterDev* it, const MomentsFinalize* fin, const CullLaunch& cl, hipStream_t s);
 // Merge `nranks` gathered moments in rank order and compute mean/std/threshold.
 hipError_t launch_finalize_moments(const Moments* gathered, int nranks, IterDev* it, MomentsFinalize fin,
                                    const CullLaunch& cl, hipStream_t s);
@@ -143,10 +146,10 @@ struct IterPublish {
 
 
 int64_t cull_num_blocks(int64_t n);
-hipError_t launch_cull_cov(const CullLaunch& a, hipStream_t s);
-// Merge the rank's partials into it->c_local; with pub (no communicator) also RMSE + publish.
-hipError_t launch_merge_cov(const CovMoments* part, int64_t nparts, const CullLaunch& cl, IterDev* it,
-                            const IterPublish* pub, hipStream_t s);
+// 3-sigma cull + covariance part sums and their last merge level into it->c_local; with pub (no
+// communicator) also RMSE + publish. With a ticket counter and at most 4096 cull blocks the last
+// block runs the last level and the publish itself (one launch instead of two).
+hipError_t launch_cull_tail(const CullLaunch& a, unsigned* ticket, const IterPublish* pub, hipStream_t s);
 // Merge `nranks` gathered covariance moments in rank order, RMSE, publish.
 hipError_t launch_finalize_cov(const CovMoments* gathered, int nranks, IterDev* it, IterPublish pub, hipStream_t s);
 

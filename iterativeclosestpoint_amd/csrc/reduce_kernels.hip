@@ -123,14 +123,182 @@ __device__ void cov_shift_store(const double* x, const double* y, const double* 
   }
 }
 
+// Fixed-shape merges of part sums, deterministic: the same n always gives the same merge tree.
+// Inner levels: block b merges items [256 b, 256 b + 256), one per thread, pairwise in LDS. Last
+// level: one block, up to 4096 items: thread t folds items t + 256 k (k < 16) in order, then the
+// block's pairwise tree.
+constexpr int kLastSpan = 4096;
+
+// The pairwise tree over the block's 256 values: at step s, thread t with t % 2s == 0 merges
+// t + s's value into its own. Steps 1..32 run inside each wave through shuffles, steps 64 and 128
+// over the four wave results: the same merges in the same order as the tree in LDS this replaced
+// (bit-identical), with 4 entries of LDS instead of 256 (so the cull blocks can run the last level
+// themselves, k_cull_cov's fused tail).
+template <typename T>
+__device__ __forceinline__ T shfl_down_T(const T& v, int s) {
+  static_assert(sizeof(T) % sizeof(double) == 0, "records of doubles");
+  T r;
+  const double* a = reinterpret_cast<const double*>(&v);
+  double* b = reinterpret_cast<double*>(&r);
+#pragma unroll
+  for (int k = 0; k < (int)(sizeof(T) / sizeof(double)); k++) b[k] = __shfl_down(a[k], s, kWave);
+  return r;
+}
+
+template <typename T, T (*Merge)(const T&, const T&), T (*Identity)()>
+__device__ __forceinline__ T block_tree(T v, T* sm) {
+  const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+#pragma unroll
+  for (int s = 1; s < kWave; s <<= 1) {
+    const T o = shfl_down_T(v, s);
+    if ((lane & (2 * s - 1)) == 0) v = Merge(v, o);
+  }
+  if (lane == 0) sm[w] = v;
+  __syncthreads();
+  const T r = Merge(Merge(sm[0], sm[1]), Merge(sm[2], sm[3]));
+  __syncthreads();
+  return r;
+}
+
+template <typename T, T (*Merge)(const T&, const T&), T (*Identity)()>
+__device__ __forceinline__ T block_tree_last(const T* in, int64_t n, T* sm) {
+  // No early exit: block_tree's barriers must be reached by every thread in uniform control flow.
+  T acc = Identity();
+#pragma unroll 4
+  for (int k = 0; k < 16; k++) {
+    const int64_t g = (int64_t)threadIdx.x + 256 * k;
+    if (g < n) acc = Merge(acc, in[g]);
+  }
+  return block_tree<T, Merge, Identity>(acc, sm);
+}
+
+// The same last level over parts another workgroup of this launch stored with sc1 (write-through)
+// stores: read with sc1 loads (L2-served, never a stale L1 line; microarch guide, hand-off row 1).
+template <typename T>
+__device__ __forceinline__ T load_sc1(const T* p) {
+  T r;
+  const double* a = reinterpret_cast<const double*>(p);
+  double* b = reinterpret_cast<double*>(&r);
+#pragma unroll
+  for (int k = 0; k < (int)(sizeof(T) / sizeof(double)); k++)
+    b[k] = __hip_atomic_load(a + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return r;
+}
+template <typename T>
+__device__ __forceinline__ void store_sc1(T* p, const T& v) {
+  const double* a = reinterpret_cast<const double*>(&v);
+  double* b = reinterpret_cast<double*>(p);
+#pragma unroll
+  for (int k = 0; k < (int)(sizeof(T) / sizeof(double)); k++)
+    __hip_atomic_store(b + k, a[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <typename T, T (*Merge)(const T&, const T&), T (*Identity)()>
+__device__ __forceinline__ T block_tree_last_sc1(const T* in, int64_t n, T* sm) {
+  T acc = Identity();
+#pragma unroll 4
+  for (int k = 0; k < 16; k++) {
+    const int64_t g = (int64_t)threadIdx.x + 256 * k;
+    if (g < n) acc = Merge(acc, load_sc1(in + g));
+  }
+  return block_tree<T, Merge, Identity>(acc, sm);
+}
+
+// "Last block done": thread 0 stores the block's part (sc1), waits for the store, then takes a
+// ticket (agent-scope atomic adds, relaxed); the block whose ticket is the last one merges every
+// part (sc1 loads, after the barrier that tells its other waves) and resets the counters for the
+// next launch. Returns true in that block only. The hand-off needs no fence (microarch guide,
+// inter-workgroup visibility, row 1): one lane per storing workgroup signals after its vmcnt
+// wait, the consumer is the workgroup whose add came last. Saves the launch of the last level.
+// The counter is sharded by blockIdx % 8 (one 128-B line per shard, the round-robin XCD of the
+// block: speed only) with a top counter that the last arrival of each shard bumps: arrivals on
+// one device-scope counter serialise at ~12 ns each (microarch guide, fanin), which cost 15 us
+// for the 1221 cull blocks of a 1.25M shard with a single counter.
+// Fused only for small grids: every block then pays a store wait and a returned atomic before it
+// retires, and the fused cull instance holds the last level's registers (128 VGPRs: 4 waves per
+// SIMD instead of 5). Measured (one MI355X, interleaved): 100k queries (25 moment parts, 98 cull
+// blocks) -2 us per iteration; at 1221 cull blocks (a 1.25M shard) +15 us, at 2442 moment parts
+// (10M) +40 us with the registers of the device loop's step in the fused cull (since removed).
+constexpr int kFuseMaxBlocks = 256;
+constexpr int kTicketLine = 32;                      // uints per counter line (128 B)
+constexpr int kTicketWords = 9 * kTicketLine;        // top + 8 shards
+template <typename T>
+__device__ __forceinline__ bool publish_part_last(T* part, const T& mine, unsigned* ticket, int* last_s) {
+  if (threadIdx.x == 0) {
+    store_sc1(part + blockIdx.x, mine);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned g = gridDim.x, sh = blockIdx.x & 7u;
+    const unsigned in_shard = (g - sh + 7u) / 8u;  // blocks b < g with b % 8 == sh
+    unsigned* sc = ticket + kTicketLine * (1 + sh);
+    bool last = false;
+    if (__hip_atomic_fetch_add(sc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == in_shard - 1u) {
+      __hip_atomic_store(sc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned shards = g < 8u ? g : 8u;
+      if (__hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == shards - 1u) {
+        __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last = true;
+      }
+    }
+    *last_s = last ? 1 : 0;
+  }
+  __syncthreads();
+  return *last_s != 0;
+}
+
 // Residual moments of the rank's queries in fixed parts of kMomPart queries, once every search
 // kernel has written its residuals: deterministic whatever order the queries were settled in.
 // Thread t of block p holds queries p kMomPart + t + 256 e (e < kMomPer, coalesced).
 constexpr int kMomPer = 16;
 constexpr int kMomPart = 256 * kMomPer;
 
+// mean = sum/row; std = sqrt(variance/row) (icpengine.cpp:235-245); threshold rule of the caller
+__device__ void finalize_moments(IterDev* it, const Moments& g, const MomentsFinalize& f) {
+  it->m_global = g;
+  const double mean = g.mean;
+  const double sd = __builtin_sqrt(g.m2 / g.n);
+  it->mean = mean;
+  it->sd = sd;
+  it->thr = cull_threshold(mean, sd, f.k_sigma, f.iter, f.engine_rules);
+}
+
+// The last level of the residual moments: the merged part sums -> (count, mean, M2) in
+// it->m_local; with finalize (one rank, no communicator) also mean/std/threshold and the cull's
+// pair shift. Run by k_merge_moments_last or by k_moments' last block (identical bits: the same
+// tree over the same parts).
+struct MomTail {
+  unsigned* ticket;  // non-null: k_moments' last block runs the last level (<= kLastSpan parts)
+  IterDev* it;
+  MomentsFinalize fin;
+  int finalize;
+  CullLaunch cl;
+};
+__device__ void moments_last(const MomSums& r, double c, const MomTail& t) {
+  __shared__ double thr_s;
+  if (threadIdx.x == 0) {
+    Moments m = moments_identity();
+    if (r.n > 0.0) {
+      m.n = r.n;
+      m.mean = c + r.s1 / r.n;
+      const double m2 = r.s2 - r.s1 * (r.s1 / r.n);
+      m.m2 = m2 < 0.0 ? 0.0 : m2;  // rounding only; NaN propagates
+      m.dmin = r.dmin;
+      m.dmax = r.dmax;
+    }
+    m.nbad = r.nbad;
+    t.it->m_local = m;
+    if (t.finalize) {
+      finalize_moments(t.it, m, t.fin);
+      thr_s = t.it->thr;
+    }
+  }
+  if (!t.finalize) return;
+  __syncthreads();
+  // the threshold, then the pair shift of the cull (the first wave)
+  cov_shift_store(t.cl.x, t.cl.y, t.cl.z, t.cl.pos, t.cl.pts, t.cl.n, thr_s, t.it);
+}
+
+template <bool FUSE>
 __global__ void __launch_bounds__(256) k_moments(const double* __restrict__ dist, int64_t n, MomSums* part,
-                                                const LoopDev* loop) {
+                                                const LoopDev* loop, MomTail tail) {
   if (loop && loop->core.done) return;  // the device loop's session finished (block-uniform)
   __shared__ double red[4 * 4];
   const double c = moment_shift_block(dist, n, red);
@@ -153,111 +321,43 @@ __global__ void __launch_bounds__(256) k_moments(const double* __restrict__ dist
   }
   block_sum<4>(v, red);
   block_minmax(mn, mx, red);
-  if (threadIdx.x == 0) {
-    MomSums m;
-    m.n = v[0];
-    m.s1 = v[1];
-    m.s2 = v[2];
-    m.dmin = mn;
-    m.dmax = mx;
-    m.nbad = v[3];
-    m.pad0 = m.pad1 = 0.0;
-    part[blockIdx.x] = m;
+  MomSums m;
+  m.n = v[0];
+  m.s1 = v[1];
+  m.s2 = v[2];
+  m.dmin = mn;
+  m.dmax = mx;
+  m.nbad = v[3];
+  m.pad0 = m.pad1 = 0.0;
+  if (!FUSE) {
+    if (threadIdx.x == 0) part[blockIdx.x] = m;
+    return;
   }
-}
-
-// Fixed-shape merges of part sums, deterministic: the same n always gives the same merge tree.
-// Inner levels: block b merges items [256 b, 256 b + 256), one per thread, pairwise in LDS. Last
-// level: one block, up to 4096 items: thread t folds items t + 256 k (k < 16) in order, then the
-// block's pairwise tree.
-constexpr int kLastSpan = 4096;
-
-template <typename T, T (*Merge)(const T&, const T&), T (*Identity)()>
-__device__ __forceinline__ T block_tree(T v, T* sm) {
-  const int t = threadIdx.x;
-  sm[t] = v;
-  __syncthreads();
-  for (int s = 1; s < 256; s <<= 1) {
-    if ((t & (2 * s - 1)) == 0) sm[t] = Merge(sm[t], sm[t + s]);
-    __syncthreads();
-  }
-  return sm[0];
-}
-
-template <typename T, T (*Merge)(const T&, const T&), T (*Identity)()>
-__device__ __forceinline__ T block_tree_last(const T* in, int64_t n, T* sm) {
-  // No early exit: block_tree's barriers must be reached by every thread in uniform control flow.
-  T acc = Identity();
-#pragma unroll 4
-  for (int k = 0; k < 16; k++) {
-    const int64_t g = (int64_t)threadIdx.x + 256 * k;
-    if (g < n) acc = Merge(acc, in[g]);
-  }
-  return block_tree<T, Merge, Identity>(acc, sm);
+  __shared__ int last_s;
+  if (!publish_part_last(part, m, tail.ticket, &last_s)) return;
+  __shared__ MomSums sm[4];
+  const MomSums r = block_tree_last_sc1<MomSums, momsum_merge, momsum_identity>(part, gridDim.x, sm);
+  moments_last(r, c, tail);
 }
 
 template <typename T, T (*Merge)(const T&, const T&), T (*Identity)()>
 __global__ void __launch_bounds__(256) k_tree_merge(const T* in, int64_t n, T* out) {
-  __shared__ T sm[256];
+  __shared__ T sm[4];
   const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const T r = block_tree<T, Merge, Identity>(g < n ? in[g] : Identity(), sm);
   if (threadIdx.x == 0) out[blockIdx.x] = r;
 }
 
-// mean = sum/row; std = sqrt(variance/row) (icpengine.cpp:235-245); threshold rule of the caller
-__device__ void finalize_moments(IterDev* it, const Moments& g, const MomentsFinalize& f) {
-  it->m_global = g;
-  const double mean = g.mean;
-  const double sd = __builtin_sqrt(g.m2 / g.n);
-  it->mean = mean;
-  it->sd = sd;
-  it->thr = cull_threshold(mean, sd, f.k_sigma, f.iter, f.engine_rules);
-}
 
-// Last level of the rank's moments: the summed part -> (count, mean, M2) in it->m_local; with fin
-// (one rank, no communicator) also the statistics.
+// Last level of the rank's moments as its own launch (more than kLastSpan parts after the inner
+// levels, or no ticket).
 __global__ void __launch_bounds__(256) k_merge_moments_last(const MomSums* in, int64_t n, const double* dist,
-                                                           int64_t nq, IterDev* it, MomentsFinalize fin, int finalize,
-                                                           CullLaunch cl) {
-  __shared__ MomSums sm[256];
+                                                           int64_t nq, MomTail tail) {
+  __shared__ MomSums sm[4];
   __shared__ double shs[1];
   const double c = moment_shift_block(dist, nq, shs);
   const MomSums r = block_tree_last<MomSums, momsum_merge, momsum_identity>(in, n, sm);
-  if (finalize) {
-    // the threshold, then the pair shift of the cull (its first wave)
-    __shared__ double thr_s;
-    if (threadIdx.x == 0) {
-      Moments m = moments_identity();
-      if (r.n > 0.0) {
-        m.n = r.n;
-        m.mean = c + r.s1 / r.n;
-        const double m2 = r.s2 - r.s1 * (r.s1 / r.n);
-        m.m2 = m2 < 0.0 ? 0.0 : m2;
-        m.dmin = r.dmin;
-        m.dmax = r.dmax;
-      }
-      m.nbad = r.nbad;
-      it->m_local = m;
-      finalize_moments(it, m, fin);
-      thr_s = it->thr;
-    }
-    __syncthreads();
-    cov_shift_store(cl.x, cl.y, cl.z, cl.pos, cl.pts, cl.n, thr_s, it);
-    return;
-  }
-  if (threadIdx.x == 0) {
-    Moments m = moments_identity();
-    if (r.n > 0.0) {
-      m.n = r.n;
-      m.mean = c + r.s1 / r.n;
-      const double m2 = r.s2 - r.s1 * (r.s1 / r.n);
-      m.m2 = m2 < 0.0 ? 0.0 : m2;  // rounding only; NaN propagates
-      m.dmin = r.dmin;
-      m.dmax = r.dmax;
-    }
-    m.nbad = r.nbad;
-    it->m_local = m;
-  }
+  moments_last(r, c, tail);
 }
 
 __global__ void __launch_bounds__(64) k_finalize_moments(const Moments* gathered, int nranks, IterDev* it,
@@ -316,6 +416,9 @@ __device__ void loop_step(LoopDev* L, const IterDev& r, LoopRec* out) {
 // stores to be acknowledged, then thread 0 stores the sequence word. No system-scope release
 // fence: it would write back the whole L2, which the search has just dirtied with megabytes. The
 // list sizes ride along (pad[0..2]) and are reset for the next search.
+// LOOP = false: an instance without the device loop's step (the session decisions and the 3x3
+// SVD): the cull kernel's fused tail, whose registers count for every cull block.
+template <bool LOOP = true>
 __device__ void finalize_cov_publish(IterDev* it, const CovMoments& g, IterPublish pub, IterDev* rec) {
   constexpr int kWords = (int)(sizeof(IterDev) / sizeof(double)) - 1;  // all but pad[3], the flag
   static_assert(offsetof(IterDev, pad) + 3 * sizeof(double) == kWords * sizeof(double), "flag is the last word");
@@ -333,9 +436,9 @@ __device__ void finalize_cov_publish(IterDev* it, const CovMoments& g, IterPubli
     for (int k = 0; k < 5; k++) pub.lists[k] = 0u;  // + the half list of the wave search
     it->c_global = rec->c_global;
     it->rmse = rec->rmse;
-    if (pub.loop) loop_step(pub.loop, *rec, pub.rec);
+    if (LOOP && pub.loop) loop_step(pub.loop, *rec, pub.rec);
   }
-  if (pub.loop) return;  // the device loop: the host reads the batch's records after it
+  if (LOOP && pub.loop) return;  // the device loop: the host reads the batch's records after it
   __syncthreads();
   double* dst = reinterpret_cast<double*>(pub.host);
   for (int k = threadIdx.x; k < kWords; k += blockDim.x)
@@ -345,14 +448,16 @@ __device__ void finalize_cov_publish(IterDev* it, const CovMoments& g, IterPubli
   if (threadIdx.x == 0) __hip_atomic_store(&pub.host->pad[3], pub.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-__global__ void __launch_bounds__(256) k_merge_cov_last(const CovSums* in, int64_t n, CullLaunch cl, IterDev* it,
-                                                       IterPublish pub, int finalize) {
-  __shared__ CovSums sm[256];
+// The last level of the covariance sums: the merged part sums -> it->c_local; with finalize (one
+// rank) also RMSE and the publish. Run by k_merge_cov_last or by k_cull_cov's last block.
+struct CovTail {
+  unsigned* ticket;  // non-null: k_cull_cov's last block runs the last level (<= kLastSpan blocks)
+  IterPublish pub;
+  int finalize;
+};
+template <bool LOOP>
+__device__ void cov_last(const CovSums& r, const IterDev* shift_src, IterDev* it, const CovTail& t) {
   __shared__ IterDev rec;
-  double sh[6];
-#pragma unroll
-  for (int k = 0; k < 6; k++) sh[k] = it->cshift[k];
-  const CovSums r = block_tree_last<CovSums, covsum_merge, covsum_identity>(in, n, sm);
   __shared__ CovMoments res;
   if (threadIdx.x == 0) {
     CovMoments m = cov_identity();
@@ -363,8 +468,8 @@ __global__ void __launch_bounds__(256) k_merge_cov_last(const CovSums* in, int64
       for (int k = 0; k < 3; k++) {
         da[k] = r.sa[k] / r.n;
         db[k] = r.sb[k] / r.n;
-        m.ma[k] = sh[k] + da[k];
-        m.mb[k] = sh[3 + k] + db[k];
+        m.ma[k] = shift_src->cshift[k] + da[k];
+        m.mb[k] = shift_src->cshift[3 + k] + db[k];
       }
       for (int i = 0; i < 3; i++)
         for (int j = 0; j < 3; j++) m.c[3 * i + j] = r.sab[3 * i + j] - r.n * (da[i] * db[j]);
@@ -372,9 +477,15 @@ __global__ void __launch_bounds__(256) k_merge_cov_last(const CovSums* in, int64
     it->c_local = m;
     res = m;
   }
-  if (!finalize) return;
+  if (!t.finalize) return;
   __syncthreads();
-  finalize_cov_publish(it, res, pub, &rec);
+  finalize_cov_publish<LOOP>(it, res, t.pub, &rec);
+}
+
+__global__ void __launch_bounds__(256) k_merge_cov_last(const CovSums* in, int64_t n, IterDev* it, CovTail tail) {
+  __shared__ CovSums sm[4];
+  const CovSums r = block_tree_last<CovSums, covsum_merge, covsum_identity>(in, n, sm);
+  cov_last<true>(r, it, it, tail);
 }
 
 __global__ void __launch_bounds__(64) k_finalize_cov(const CovMoments* gathered, int nranks, IterDev* it,
@@ -393,7 +504,11 @@ __global__ void __launch_bounds__(64) k_finalize_cov(const CovMoments* gathered,
 // operations on the same operands give its bits again (8 of 68 B per query not streamed).
 constexpr int kCullPer = 4;
 
-__global__ void __launch_bounds__(256) k_cull_cov(CullLaunch a) {
+// FUSE: the last block runs the last merge level and (finalize) the publish; not with the device
+// loop (whose step would put the SVD's registers into every cull block): that one keeps
+// k_merge_cov_last.
+template <bool FUSE>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k_cull_cov(CullLaunch a, CovTail tail) {
   if (a.loop && a.loop->core.done) return;  // the device loop's session finished (block-uniform)
   __shared__ double red[4 * 17];
   const double thr = a.it->thr;
@@ -445,18 +560,25 @@ __global__ void __launch_bounds__(256) k_cull_cov(CullLaunch a) {
     }
   }
   block_sum<17>(v, red);
-  if (threadIdx.x == 0) {
-    CovSums m;
-    m.n = v[0];
-    m.sum_d2 = v[1];
-    for (int k = 0; k < 3; k++) {
-      m.sa[k] = v[2 + k];
-      m.sb[k] = v[5 + k];
-      m.pad[k] = 0.0;
-    }
-    for (int k = 0; k < 9; k++) m.sab[k] = v[8 + k];
-    reinterpret_cast<CovSums*>(a.part)[blockIdx.x] = m;
+  CovSums m;
+  m.n = v[0];
+  m.sum_d2 = v[1];
+  for (int k = 0; k < 3; k++) {
+    m.sa[k] = v[2 + k];
+    m.sb[k] = v[5 + k];
+    m.pad[k] = 0.0;
   }
+  for (int k = 0; k < 9; k++) m.sab[k] = v[8 + k];
+  CovSums* part = reinterpret_cast<CovSums*>(a.part);
+  if (!FUSE) {
+    if (threadIdx.x == 0) part[blockIdx.x] = m;
+    return;
+  }
+  __shared__ int last_s;
+  if (!publish_part_last(part, m, tail.ticket, &last_s)) return;
+  __shared__ CovSums sm[4];
+  const CovSums r = block_tree_last_sc1<CovSums, covsum_merge, covsum_identity>(part, gridDim.x, sm);
+  cov_last<false>(r, a.it, const_cast<IterDev*>(a.it), tail);
 }
 
 template <typename T, T (*Merge)(const T&, const T&), T (*Identity)()>
@@ -478,6 +600,8 @@ const T* merge_to_last_span(const T* part, int64_t* nparts, hipStream_t s) {
 
 }  // namespace
 
+int ticket_words() { return 2 * kTicketWords; }
+
 // Partial buffers hold the block partials followed by the merge scratch (merge_scratch_entries).
 int64_t merge_scratch_entries(int64_t nparts) {
   int64_t total = 0;
@@ -487,19 +611,20 @@ int64_t merge_scratch_entries(int64_t nparts) {
 
 int64_t moments_num_parts(int64_t n) { return (n + kMomPart - 1) / kMomPart; }
 
-hipError_t launch_moments(const double* dist, int64_t n, Moments* part, const LoopDev* loop, hipStream_t s) {
-  if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_moments, dim3((unsigned)moments_num_parts(n)), dim3(256), 0, s, dist, n,
-                     reinterpret_cast<MomSums*>(part), loop);
-  return hipGetLastError();
-}
-
-hipError_t launch_merge_moments(const Moments* part, int64_t nparts, const double* dist, int64_t nq, IterDev* it,
-                                const MomentsFinalize* fin, const CullLaunch& cl, hipStream_t s) {
-  const MomSums* cur = merge_to_last_span<MomSums, momsum_merge, momsum_identity>(
-      reinterpret_cast<const MomSums*>(part), &nparts, s);
-  hipLaunchKernelGGL(k_merge_moments_last, dim3(1), dim3(256), 0, s, cur, nparts, dist, nq, it,
-                     fin ? *fin : MomentsFinalize{0.0, 0, 0}, fin ? 1 : 0, cl);
+hipError_t launch_moments_tail(const double* dist, int64_t n, Moments* part, const LoopDev* loop, unsigned* ticket,
+                               IterDev* it, const MomentsFinalize* fin, const CullLaunch& cl, hipStream_t s) {
+  const int64_t nparts = moments_num_parts(n);
+  MomTail tail{nullptr, it, fin ? *fin : MomentsFinalize{0.0, 0, 0}, fin ? 1 : 0, cl};
+  MomSums* sums = reinterpret_cast<MomSums*>(part);
+  if (ticket && nparts >= 1 && nparts <= kFuseMaxBlocks) {  // one launch: the last block merges
+    tail.ticket = ticket;
+    hipLaunchKernelGGL(k_moments<true>, dim3((unsigned)nparts), dim3(256), 0, s, dist, n, sums, loop, tail);
+    return hipGetLastError();
+  }
+  if (n > 0) hipLaunchKernelGGL(k_moments<false>, dim3((unsigned)nparts), dim3(256), 0, s, dist, n, sums, loop, tail);
+  int64_t np = nparts;
+  const MomSums* cur = merge_to_last_span<MomSums, momsum_merge, momsum_identity>(sums, &np, s);
+  hipLaunchKernelGGL(k_merge_moments_last, dim3(1), dim3(256), 0, s, cur, np, dist, n, tail);
   return hipGetLastError();
 }
 
@@ -511,18 +636,19 @@ hipError_t launch_finalize_moments(const Moments* gathered, int nranks, IterDev*
 
 int64_t cull_num_blocks(int64_t n) { return (n + 256 * kCullPer - 1) / (256 * kCullPer); }
 
-hipError_t launch_cull_cov(const CullLaunch& a, hipStream_t s) {
-  if (a.n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_cull_cov, dim3((unsigned)cull_num_blocks(a.n)), dim3(256), 0, s, a);
-  return hipGetLastError();
-}
-
-hipError_t launch_merge_cov(const CovMoments* part, int64_t nparts, const CullLaunch& cl, IterDev* it,
-                            const IterPublish* pub, hipStream_t s) {
+hipError_t launch_cull_tail(const CullLaunch& a, unsigned* ticket, const IterPublish* pub, hipStream_t s) {
+  const int64_t nb = cull_num_blocks(a.n);
+  CovTail tail{nullptr, pub ? *pub : IterPublish{nullptr, nullptr, 0.0, nullptr, nullptr}, pub ? 1 : 0};
+  if (ticket && nb >= 1 && nb <= kFuseMaxBlocks && !a.loop) {  // one launch: the last block merges and publishes
+    tail.ticket = ticket;
+    hipLaunchKernelGGL(k_cull_cov<true>, dim3((unsigned)nb), dim3(256), 0, s, a, tail);
+    return hipGetLastError();
+  }
+  if (a.n > 0) hipLaunchKernelGGL(k_cull_cov<false>, dim3((unsigned)nb), dim3(256), 0, s, a, tail);
+  int64_t np = nb;
   const CovSums* cur = merge_to_last_span<CovSums, covsum_merge, covsum_identity>(
-      reinterpret_cast<const CovSums*>(part), &nparts, s);
-  hipLaunchKernelGGL(k_merge_cov_last, dim3(1), dim3(256), 0, s, cur, nparts, cl, it,
-                     pub ? *pub : IterPublish{nullptr, nullptr, 0.0, nullptr, nullptr}, pub ? 1 : 0);
+      reinterpret_cast<const CovSums*>(a.part), &np, s);
+  hipLaunchKernelGGL(k_merge_cov_last, dim3(1), dim3(256), 0, s, cur, np, const_cast<IterDev*>(a.it), tail);
   return hipGetLastError();
 }
 
