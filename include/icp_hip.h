@@ -156,6 +156,7 @@ typedef struct icp_hip_config {
 #define ICP_DBG_WALK_MOVED 24   /* waves with a record of this generation that walked because
                                     their box left B+                                        */
 #define ICP_DBG_WALK_LOOSE 25   /* waves whose box lay inside B+ but walked because B+ was loose */
+#define ICP_DBG_GROUP_POINTS 26 /* fp32 scan: points staged, summed over the scan groups       */
 #define ICP_DBG_SLOTS 32
 
 typedef struct icp_hip_ctx icp_hip_ctx;

@@ -829,6 +829,7 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
           wstore = false;
         }
       }
+      if (kDbg && a.dbg && lane == 0) atomicAdd(&a.dbg[26], (unsigned long long)scanned_pts);  // sum over groups
       const float s2 = __uint_as_float(__float_as_uint(k2) & ~63u);  // <= the second-smallest value
       // fp64 distance of the fp32 winner, exactly as the leaf scan computes it (octree.cpp:139-144)
       double b64 = __builtin_inf();
