@@ -1,9 +1,12 @@
 #!/bin/bash
 # Profile the bench command with rocprofv3 (kernel trace + stats; then separate PMC passes).
 # usage (on the GPU box, from the repo root): bash tools/profile_bench.sh TAG [N]
+# STEPS / WARMUP (default 20 / 5: the driver's own arguments) set the timed window of every pass.
 set -u
 TAG=${1:-r01}
 N=${2:-10000000}
+STEPS=${STEPS:-20}
+WARMUP=${WARMUP:-5}
 REPO=$(pwd)
 OUT=$REPO/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
@@ -11,13 +14,13 @@ export TMPDIR=/tmp
 BENCH="$REPO/bench.py --points $N --no-cpu-baseline --no-parity --no-registration"
 cd /tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o "$TAG" -- \
-  python3 $BENCH --steps 200 --warmup 5 > "$OUT/bench_traced.json" 2> "$OUT/trace.err" || exit $?
+  python3 $BENCH --steps $STEPS --warmup $WARMUP > "$OUT/bench_traced.json" 2> "$OUT/trace.err" || exit $?
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o "$TAG" -- \
-  python3 $BENCH --steps 50 --warmup 5 > /dev/null 2> "$OUT/pmc_fetch.err" || exit $?
+  python3 $BENCH --steps $STEPS --warmup $WARMUP > /dev/null 2> "$OUT/pmc_fetch.err" || exit $?
 timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o "$TAG" -- \
-  python3 $BENCH --steps 50 --warmup 5 > /dev/null 2> "$OUT/pmc_write.err" || exit $?
+  python3 $BENCH --steps $STEPS --warmup $WARMUP > /dev/null 2> "$OUT/pmc_write.err" || exit $?
 timeout -k 10 600 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv -d "$OUT/pmc_l2" -o "$TAG" -- \
-  python3 $BENCH --steps 50 --warmup 5 > /dev/null 2> "$OUT/pmc_l2.err" || exit $?
+  python3 $BENCH --steps $STEPS --warmup $WARMUP > /dev/null 2> "$OUT/pmc_l2.err" || exit $?
 cd "$REPO"
 python3 tools/pmc_traffic.py "$OUT" "$N" 1 > "$OUT/traffic.json"
 cat "$OUT/traffic.json"
