@@ -68,8 +68,10 @@ typedef struct icp_hip_config {
                              blocks, dealt round-robin over the XCDs; 0: hardware order  dflt 256 */
   int32_t scan_groups;    /* 1, 2 or 4: the fp32 filter scan of a wave splits its lanes into this
                              many kd sub-buckets, each scanning only the candidates inside its
-                             own box (fewer distance evaluations per query, more staging
-                             work: 7 % faster at 2, slower at 4 on config 4)             dflt 2 */
+                             own box; a wave that reuses its cache record stages its groups'
+                             candidates across its chunks and scans once (fewer evaluations per
+                             query against more staging work: at 4, 29 point pairs per wave
+                             instead of 48 at 2; search 4-7 % faster on config 4)     dflt 4 */
   int32_t candidate_cache;  /* 1: each wave of the iterate's search keeps the candidate list of
                                its search box B enlarged by candidate_margin (1/256 units of B's
                                largest half-extent per side), and the next iterate reuses it
@@ -157,6 +159,9 @@ typedef struct icp_hip_config {
                                     their box left B+                                        */
 #define ICP_DBG_WALK_LOOSE 25   /* waves whose box lay inside B+ but walked because B+ was loose */
 #define ICP_DBG_GROUP_POINTS 26 /* fp32 scan: points staged, summed over the scan groups       */
+#define ICP_DBG_EXIT_FWD 27     /* walk_moved waves whose box left B+ on the side it moves to  */
+#define ICP_DBG_EXIT_BACK 28    /* ... on the side opposite to its motion                       */
+#define ICP_DBG_EXIT_GREW 29    /* ... and whose box is wider than B+ on some axis              */
 #define ICP_DBG_SLOTS 32
 
 typedef struct icp_hip_ctx icp_hip_ctx;

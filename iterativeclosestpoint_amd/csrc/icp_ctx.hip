@@ -140,7 +140,7 @@ void icp_hip_config_default(icp_hip_config* cfg) {
   cfg->join_factor = 3.0;
   cfg->debug_counters = 0;
   cfg->xcd_blocks = 256;
-  cfg->scan_groups = 2;
+  cfg->scan_groups = 4;
   cfg->candidate_cache = 1;
   cfg->candidate_margin = 16;
   cfg->candidate_loose = 190;

@@ -106,6 +106,7 @@ constexpr int kWavePoints = 1024;  // candidate list area (up to kWaveCandCap id
 static_assert(kWaveCandCap <= kWavePoints, "candidate list");
 constexpr int kWaveLds = kWaveQueue * 4 + kWavePoints * 4;  // 5 KB per wave
 static_assert(kWaveQueue * 4 >= 64 * 16 && kWaveQueue * 4 >= 32 * 32, "staging area aliases the stack");
+static_assert(kWaveQueue * 4 + kWavePoints * 4 >= 128 * 16, "a reusing wave stages 128 points (stack + list area)");
 
 // fp32 radius r >= sqrt(u) (1 + 2^-40) + amax 2^-45 (the ball of the wave search's certificate):
 // the fp32 square root rounded up ((float) rounds by <= 2^-24, v_sqrt_f32 is within 1 ulp, each
@@ -517,6 +518,24 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
       if (kDbg && a.dbg && lane == 0 && !reuse && (uint32_t)(cg >> 32) == a.wc_gen) {
         const bool inside = blx >= hlx && bly >= hly && blz >= hlz && bhx <= hhx && bhy <= hhy && bhz <= hhz;
         atomicAdd(&a.dbg[inside ? 25 : 24], 1ull);
+        if (!inside && APPLY) {
+          // which side B left B+ by, against this iterate's motion of B's centre: the side it
+          // moves to (27) or the opposite side (28); and whether B is larger than B+ on an axis
+          // (29: its balls grew past the margins)
+          const double* T = a.loop ? a.loop->core.T : a.T;
+          const double c[3] = {(blx + bhx) * 0.5, (bly + bhy) * 0.5, (blz + bhz) * 0.5};
+          const double lo[3] = {blx, bly, blz}, hi[3] = {bhx, bhy, bhz}, plo[3] = {hlx, hly, hlz}, phi[3] = {hhx, hhy, hhz};
+          bool fwd = false, back = false, grew = false;
+          for (int k = 0; k < 3; k++) {
+            const double e = (((T[4 * k] * c[0] + T[4 * k + 1] * c[1]) + T[4 * k + 2] * c[2]) + T[4 * k + 3]) - c[k];
+            if (lo[k] < plo[k]) (e < 0.0 ? fwd : back) = true;
+            if (hi[k] > phi[k]) (e > 0.0 ? fwd : back) = true;
+            grew = grew || (hi[k] - lo[k]) > (phi[k] - plo[k]);
+          }
+          if (fwd) atomicAdd(&a.dbg[27], 1ull);
+          if (back) atomicAdd(&a.dbg[28], 1ull);
+          if (grew) atomicAdd(&a.dbg[29], 1ull);
+        }
       }
       if (reuse) {
         nleaf = (int)(uint32_t)cg;
@@ -672,9 +691,15 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
         gh[g][1] = uni((ghi[g][1] + doy) + mg);
         gh[g][2] = uni((ghi[g][2] + doz) + mg);
       }
-      constexpr int S = 64 / NG;  // lanes of a group = points of a group's segment per round
-      const int gq = lane / S;    // this lane's group
-      // staging area: NG segments of S points, in pairs [x0 x1 y0 y1 z0 z1 w0 w1] (32 B) so that
+      constexpr int LG = 64 / NG;  // lanes of a group
+      // points of a group's segment per round: LG for a walking wave (its candidate list occupies
+      // the list area); a wave that reuses its cache record leaves the list area unused, so it
+      // stages up to 64 points per group (NG x 1 KB: the stack area and the list area) across its
+      // chunks and scans once they would overflow (usually once per wave); slots stay below 64
+      // (6 key bits)
+      const int SP = reuse ? 64 : LG;
+      const int gq = lane / LG;  // this lane's group
+      // staging area: NG segments of SP points, in pairs [x0 x1 y0 y1 z0 z1 w0 w1] (32 B) so that
       // one packed fp32 instruction (v_pk_add/mul/fma_f32) evaluates an axis of two points.
       // Pair k of group g at k NG + g: the groups interleaved (each group's pairs contiguous costs
       // two more spilled registers)
@@ -732,7 +757,7 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
               maxc = cn[g] > maxc ? cn[g] : maxc;
             }
             const int j = mask_rank(mk) - r0;
-            if (in && j >= 0 && j < S) {
+            if (in && j >= 0 && j < SP) {
               float* sp = stage32 + 8 * blk(j >> 1, g) + (j & 1);
               sp[0] = vx;
               sp[2] = vy;
@@ -746,26 +771,28 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
 #pragma unroll
         for (int g = 0; g < NG; g++) scanned_pts += cn[g];
         next();
-        for (int r0 = 0; r0 < maxc; r0 += S) {
+        for (int r0 = 0; r0 < maxc; r0 += SP) {
           if (r0 > 0) {
             wave_lds_fence();
             stage_round(r0, false);
           }
           // every segment padded to the round's even length with far points (index -1)
-          int len = maxc - r0 < S ? maxc - r0 : S;
+          int len = maxc - r0 < SP ? maxc - r0 : SP;
           len = (len + 1) & ~1;
           {
-            const int pg = lane / S, pj = lane % S;
+            const int pg = lane / LG;
             int c = cn[0];
 #pragma unroll
             for (int g = 1; g < NG; g++) c = pg == g ? cn[g] : c;
             c -= r0;
-            if (pj >= c && pj < len) {
-              float* sp = stage32 + 8 * blk(pj >> 1, pg) + (pj & 1);
-              sp[0] = 0x1p62f;
-              sp[2] = 0x1p62f;
-              sp[4] = 0x1p62f;
-              sp[6] = __int_as_float(-1);
+            for (int pj = lane % LG; pj < len; pj += LG) {
+              if (pj >= c) {
+                float* sp = stage32 + 8 * blk(pj >> 1, pg) + (pj & 1);
+                sp[0] = 0x1p62f;
+                sp[2] = 0x1p62f;
+                sp[4] = 0x1p62f;
+                sp[6] = __int_as_float(-1);
+              }
             }
           }
           wave_lds_fence();
@@ -773,7 +800,7 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
           const float k1_in = k1;
           const int mp = len >> 1;
           if (kDbg && a.dbg && lane == 0) {
-            atomicAdd(&a.dbg[9], (unsigned long long)(maxc - r0 < S ? maxc - r0 : S));
+            atomicAdd(&a.dbg[9], (unsigned long long)(maxc - r0 < SP ? maxc - r0 : SP));
             atomicAdd(&a.dbg[10], (unsigned long long)mp);
             atomicAdd(&a.dbg[11], 1ull);
           }
@@ -788,13 +815,83 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
       };
       wave_lds_fence();
       if (reuse) {
+        // Accumulate: each chunk's points are staged behind the previous chunks' (per group),
+        // and a scan round runs only when a group's segment would overflow, and at the end. The
+        // lockstep scan then pays max over groups of the wave's whole count once, not of every
+        // chunk's count (pairs per wave 34.6 -> ~27 at NG = 4), and fewer rounds. The next
+        // chunk's loads are issued before the current one is staged.
+        int fill[NG];
+#pragma unroll
+        for (int g = 0; g < NG; g++) fill[g] = 0;
+        auto scan_round = [&]() {
+          int maxf = 0;
+#pragma unroll
+          for (int g = 0; g < NG; g++) maxf = fill[g] > maxf ? fill[g] : maxf;
+          const int len = (maxf + 1) & ~1;
+          const int pg = lane / LG;
+          int c = fill[0];
+#pragma unroll
+          for (int g = 1; g < NG; g++) c = pg == g ? fill[g] : c;
+          for (int pj = lane % LG; pj < len; pj += LG) {
+            if (pj >= c) {
+              float* sp = stage32 + 8 * blk(pj >> 1, pg) + (pj & 1);
+              sp[0] = 0x1p62f;
+              sp[2] = 0x1p62f;
+              sp[4] = 0x1p62f;
+              sp[6] = __int_as_float(-1);
+            }
+          }
+          wave_lds_fence();
+          const float k1_in = k1;
+          const int mp = len >> 1;
+          if (kDbg && a.dbg && lane == 0) {
+            atomicAdd(&a.dbg[9], (unsigned long long)maxf);
+            atomicAdd(&a.dbg[10], (unsigned long long)mp);
+            atomicAdd(&a.dbg[11], 1ull);
+          }
+#pragma unroll 1
+          for (int k = 0; k < mp; k++) eval2(st4[kStep * k], st4[kStep * k + 1], 2u * k);
+          if (k1 != k1_in) {
+            const uint32_t sl = __float_as_uint(k1) & 63u;
+            p1 = __float_as_int(stage32[8 * blk((int)(sl >> 1), gq) + 6 + (sl & 1u)]);
+          }
+          wave_lds_fence();  // the round's reads are done before the slots are rewritten
+#pragma unroll
+          for (int g = 0; g < NG; g++) fill[g] = 0;
+        };
         float4 nx = ent0;  // loaded with the query
         for (int base = 0; base < npts; base += 64) {
           const float vx = nx.x, vy = nx.y, vz = nx.z, vw = nx.w;
-          chunk(base, vx, vy, vz, vw, [&]() {
-            if (base + 64 + lane < npts) nx = wents[base + 64 + lane];
-          });
+          if (base + 64 + lane < npts) nx = wents[base + 64 + lane];
+          const bool valid = base + lane < npts;
+          uint32_t mem = 0;  // this lane's point: member of which groups
+          int cn[NG];
+          bool over = false;
+#pragma unroll
+          for (int g = 0; g < NG; g++) {
+            const bool in = valid && vx >= gl[g][0] && vx <= gh[g][0] && vy >= gl[g][1] && vy <= gh[g][1] &&
+                            vz >= gl[g][2] && vz <= gh[g][2];
+            mem |= in ? 1u << g : 0u;
+            cn[g] = __popcll(__ballot(in));
+            over = over || fill[g] + cn[g] > SP;
+          }
+          if (over) scan_round();
+#pragma unroll
+          for (int g = 0; g < NG; g++) {
+            const bool in = (mem >> g) & 1u;
+            const int j = fill[g] + mask_rank(__ballot(in));
+            if (in) {
+              float* sp = stage32 + 8 * blk(j >> 1, g) + (j & 1);
+              sp[0] = vx;
+              sp[2] = vy;
+              sp[4] = vz;
+              sp[6] = vw;
+            }
+            fill[g] += cn[g];
+            scanned_pts += cn[g];
+          }
         }
+        scan_round();
       } else {
         int wcount = 0;  // entries stored to the cache (points inside B+)
         double4 nxtp = make_double4(0.0, 0.0, 0.0, 0.0);

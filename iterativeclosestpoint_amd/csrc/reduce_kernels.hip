@@ -219,6 +219,9 @@ __device__ __forceinline__ T block_tree_last_sc1(const T* in, int64_t n, T* sm) 
 // blocks) -2 us per iteration; at 1221 cull blocks (a 1.25M shard) +15 us, at 2442 moment parts
 // (10M) +40 us with the registers of the device loop's step in the fused cull (since removed).
 constexpr int kFuseMaxBlocks = 256;
+// the moments blocks are short and register-light: fused up to 512 parts (2M queries; at 2442
+// parts, 10M, the per-block ticket cost 5 us more than the separate launch)
+constexpr int kFuseMaxMomentParts = 512;
 constexpr int kTicketLine = 32;                      // uints per counter line (128 B)
 constexpr int kTicketWords = 9 * kTicketLine;        // top + 8 shards
 template <typename T>
@@ -616,7 +619,7 @@ hipError_t launch_moments_tail(const double* dist, int64_t n, Moments* part, con
   const int64_t nparts = moments_num_parts(n);
   MomTail tail{nullptr, it, fin ? *fin : MomentsFinalize{0.0, 0, 0}, fin ? 1 : 0, cl};
   MomSums* sums = reinterpret_cast<MomSums*>(part);
-  if (ticket && nparts >= 1 && nparts <= kFuseMaxBlocks) {  // one launch: the last block merges
+  if (ticket && nparts >= 1 && nparts <= kFuseMaxMomentParts) {  // one launch: the last block merges
     tail.ticket = ticket;
     hipLaunchKernelGGL(k_moments<true>, dim3((unsigned)nparts), dim3(256), 0, s, dist, n, sums, loop, tail);
     return hipGetLastError();

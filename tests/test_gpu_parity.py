@@ -259,7 +259,7 @@ def test_fallback_share_small_on_scans(icp, gpu_ctx):
                                    (300_000, {"cell_starts": 0, "scan32": 0}),
                                    (1_000_000, {"join_factor": 1e6}),
                                    (300_000, {"octree_builder": 1}),
-                                   (1_000_000, {"scan_groups": 1}), (1_000_000, {"scan_groups": 4}),
+                                   (1_000_000, {"scan_groups": 1}), (1_000_000, {"scan_groups": 2}),
                                    (300_000, {"xcd_blocks": 0}),
                                    (1_000_000, {"candidate_cache": 0}), (300_000, {"candidate_margin": 0}),
                                    (300_000, {"candidate_margin": 256}),
