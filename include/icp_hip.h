@@ -121,6 +121,12 @@ typedef struct icp_hip_config {
                               wave's queries the same way for many iterates: a record then lasts
                               until they have moved that far), in [0, 64]; 0: symmetric margin
                               only                                                       dflt 8 */
+  int32_t fused_cull;      /* 1: from a source's second iterate on, the wave search also sums the
+                              covariance terms of its pairs below a band around the previous
+                              iterate's threshold, and the cull pass only settles the band and the
+                              waves the search left to its other paths (icp_hip_last_cull_path);
+                              0: every cull is a full pass. The same valid pairs either way; the
+                              sums differ in their order only                             dflt 1 */
 } icp_hip_config;
 
 /* Slots of icp_hip_debug_counters (summed over the last iterate's search launches). */
@@ -162,6 +168,9 @@ typedef struct icp_hip_config {
 #define ICP_DBG_EXIT_FWD 27     /* walk_moved waves whose box left B+ on the side it moves to  */
 #define ICP_DBG_EXIT_BACK 28    /* ... on the side opposite to its motion                       */
 #define ICP_DBG_EXIT_GREW 29    /* ... and whose box is wider than B+ on some axis              */
+#define ICP_DBG_FZ_RECOMPUTE 30 /* waves whose covariance record the cull recomputes (queries
+                                   left to the other searches)                                 */
+#define ICP_DBG_FZ_BAND 31      /* queries in the band around the previous threshold           */
 #define ICP_DBG_SLOTS 32
 
 typedef struct icp_hip_ctx icp_hip_ctx;
@@ -322,6 +331,14 @@ int icp_hip_last_timing(icp_hip_ctx* ctx, double* nn_kernel_ms, double* iterate_
  * NaN for an iterate that config.timing_stride left untimed.
  * Waits for them to finish. */
 int icp_hip_timings(icp_hip_ctx* ctx, int k, double* nn_kernel_ms, double* iterate_device_ms);
+
+/* Which pass produced the last host-published iterate's covariance sums: 1 = the wave search
+ * summed its pairs below a band around the previous threshold and the cull pass only settled the
+ * band and the waves the search left unfinished; 0 = a full cull pass (a source's first iterate,
+ * a threshold outside the band, the reference-order search). The statistics are the same either
+ * way up to the summation order. A multi-device context reports 1 when every member did.
+ * ICP_HIP_ENOTREADY before the first iterate of a source. */
+int icp_hip_last_cull_path(icp_hip_ctx* ctx, int32_t* fused);
 
 /* The wave search's diagnostic counters of the last iterate (ICP_DBG_* slots); zeros unless the
  * context was created with debug_counters = 1. */

@@ -34,7 +34,7 @@ DBG_NAMES = {0: "waves", 1: "overflow_waves", 2: "not_joined", 3: "not_covered",
              21: "start_nodes", 20: "winner_prev_waves", 22: "winner_prev", 23: "winner_lanes",
              18: "prev_cert_waves", 19: "prev_cert_lanes", 16: "halves", 17: "reused_entries",
              24: "walk_moved", 25: "walk_loose", 26: "group_points", 27: "exit_fwd", 28: "exit_back",
-             29: "exit_grew"}
+             29: "exit_grew", 30: "fz_recompute", 31: "fz_band"}
 
 _P = C.c_void_p
 _D = C.POINTER(C.c_double)
@@ -72,7 +72,7 @@ class HipConfig(C.Structure):
         ("xcd_blocks", C.c_int32), ("scan_groups", C.c_int32), ("candidate_cache", C.c_int32),
         ("candidate_margin", C.c_int32), ("certify_prev", C.c_int32), ("query_order", C.c_int32),
         ("overflow_halves", C.c_int32), ("device_loop", C.c_int32), ("timing_stride", C.c_int32),
-        ("candidate_loose", C.c_int32), ("candidate_lead", C.c_int32),
+        ("candidate_loose", C.c_int32), ("candidate_lead", C.c_int32), ("fused_cull", C.c_int32),
     ]
 
 
@@ -162,6 +162,7 @@ SIGNATURES = {
     "icp_hip_traversal_counts": (C.c_int, [_P, _D, _D]),
     "icp_hip_target_info": (C.c_int, [_P, C.POINTER(C.c_int64), C.POINTER(C.c_int64), _I32, _I32]),
     "icp_hip_last_timing": (C.c_int, [_P, _D, _D]),
+    "icp_hip_last_cull_path": (C.c_int, [_P, _I32]),
     "icp_hip_timings": (C.c_int, [_P, C.c_int, _P, _P]),
     "icp_hip_target_build_info": (C.c_int, [_P, _I32, _D]),
     "icp_hip_copy_target": (C.c_int, [_P, _P, _P, _P, _P, _P, _P]),
@@ -438,6 +439,13 @@ class Context:
         a, b = C.c_double(), C.c_double()
         _check(lib().icp_hip_last_timing(self._h, C.byref(a), C.byref(b)))
         return a.value, b.value
+
+    def last_cull_path(self) -> int:
+        """1: the last iterate's covariance sums came from the wave search's records + the band
+        pairs; 0: a full cull pass (icp_hip_last_cull_path)."""
+        f = C.c_int32()
+        _check(lib().icp_hip_last_cull_path(self._h, C.byref(f)))
+        return f.value
 
     def timings(self, k: int):
         """(search kernel ms, iterate device ms) of each of the last k iterates, oldest first."""

@@ -83,7 +83,16 @@ static void free_source(icp_hip_ctx* c) {
   dfree(c->wc_ents);
   dfree(c->mparts);
   dfree(c->cparts);
+  dfree(c->wstat);
   c->n_src = 0;
+}
+
+// No band for the next iterate's search (a new source or target): its cull pass does it all.
+static hipError_t reset_band(icp_hip_ctx* c) {
+  c->last_cull_path = -1;
+  char* base = reinterpret_cast<char*>(c->it);
+  return hipMemsetAsync(base + offsetof(IterDev, fz_lo), 0, offsetof(IterDev, cull_mode) - offsetof(IterDev, fz_lo),
+                        c->stream);
 }
 
 static void free_target(icp_hip_ctx* c) {
@@ -145,6 +154,7 @@ void icp_hip_config_default(icp_hip_config* cfg) {
   cfg->candidate_margin = 16;
   cfg->candidate_loose = 190;
   cfg->candidate_lead = 8;
+  cfg->fused_cull = 1;
   cfg->overflow_halves = 1;
   cfg->device_loop = 0;
   cfg->timing_stride = 0;
@@ -172,6 +182,7 @@ int icp_hip_create_ex(icp_hip_ctx** out, int device, const icp_hip_config* cfg) 
   if (conf.candidate_loose < 100 || conf.candidate_loose > 100000)
     return fail(ICP_HIP_EINVAL, "config: candidate_loose out of [100, 100000]");
   if (conf.candidate_lead < 0 || conf.candidate_lead > 64) return fail(ICP_HIP_EINVAL, "config: candidate_lead out of [0, 64]");
+  if (conf.fused_cull < 0 || conf.fused_cull > 1) return fail(ICP_HIP_EINVAL, "config: fused_cull must be 0 or 1");
   if (conf.overflow_halves != 0 && conf.overflow_halves != 1) return fail(ICP_HIP_EINVAL, "config: overflow_halves must be 0 or 1");
   if (conf.query_order != 0 && conf.query_order != 1) return fail(ICP_HIP_EINVAL, "config: query_order must be 0 or 1");
   if (conf.certify_prev < 0 || conf.certify_prev > 3) return fail(ICP_HIP_EINVAL, "config: certify_prev out of [0, 3]");
@@ -375,6 +386,7 @@ int icp_hip_set_target(icp_hip_ctx* c, const double* xyz, int64_t n, int max_poi
   if (n > (int64_t)0x7fffffff) return fail(ICP_HIP_EINVAL, "target size out of range (int32 indices, as the reference)");
   HIP_TRY(hipSetDevice(c->device));
   free_target(c);
+  HIP_TRY(reset_band(c));
   hipEvent_t e0 = c->ev_it0, e1 = c->ev_it1;
   HIP_TRY(hipEventRecord(e0, c->stream));
   const bool on_device = max_depth <= kGpuBuildMaxDepth && c->cfg.octree_builder == ICP_BUILD_AUTO;
@@ -539,6 +551,11 @@ int icp_hip_set_source(icp_hip_ctx* c, const double* xyz, int64_t n) {
   c->wc_gen++;
   HIP_TRY(dalloc(&c->mparts, (size_t)(c->nb_mom + merge_scratch_entries(c->nb_mom))));
   HIP_TRY(dalloc(&c->cparts, (size_t)(c->nb_cull + merge_scratch_entries(c->nb_cull))));
+  if (n > 0 && c->cfg.fused_cull && dalloc(&c->wstat, (size_t)((n + 63) / 64)) != hipSuccess) {
+    (void)hipGetLastError();  // without the records every cull is a full pass (identical results)
+    dfree(c->wstat);
+  }
+  HIP_TRY(reset_band(c));
   if (n == 0) return ICP_HIP_OK;
   // Spatially compact query order (kd buckets of 64 = one wave): on the device from the uploaded
   // cloud (query_order_gpu.hip), or on the host (config query_order = 1)
@@ -602,6 +619,9 @@ static int enqueue_iterate(icp_hip_ctx* c, const double* T_apply, bool apply, in
   a.wc_margin = c->cfg.candidate_margin / 256.0;
   a.wc_loose = c->cfg.candidate_loose / 100.0;
   a.wc_lead = (double)c->cfg.candidate_lead;
+  // the wave records of the fused covariance sums (the wave search only)
+  a.wstat = (c->cfg.search == ICP_SEARCH_CERTIFIED && c->cfg.fused_cull) ? c->wstat : nullptr;
+  a.fz = c->it;
   if (!c->lists_zero) HIP_TRY(hipMemsetAsync(c->fb_count, 0, 8 * sizeof(unsigned int), s));
   c->lists_zero = false;
   if (c->dbg) HIP_TRY(hipMemsetAsync(c->dbg, 0, ICP_DBG_SLOTS * sizeof(unsigned long long), s));
@@ -629,6 +649,8 @@ static int enqueue_iterate(icp_hip_ctx* c, const double* T_apply, bool apply, in
   cl.it = c->it;
   cl.part = c->cparts;
   cl.n = c->n_src;
+  cl.dist = c->dist;
+  cl.wstat = a.wstat;
   HIP_TRY(launch_moments_tail(c->dist, c->n_src, c->mparts, loop, c->tickets, c->it, multi ? nullptr : &fin, cl, s));
   if (multi) {
     const int rc = all_gather_record(c, reinterpret_cast<const double*>(&c->it->m_local),
@@ -701,6 +723,7 @@ int icp_hip_iterate(icp_hip_ctx* c, const double* T_apply, int iter, int rules, 
   c->lists_zero = true;
   for (int k = 0; k < 3; k++) c->last_lists[k] = (unsigned int)c->h_it->pad[k];
   const IterDev& h = *c->h_it;
+  c->last_cull_path = h.cull_mode != 0.0 ? 1 : 0;
   out->n = (int64_t)h.m_global.n;
   out->mean = h.mean;
   out->std = h.sd;
@@ -966,6 +989,14 @@ int icp_hip_last_timing(icp_hip_ctx* c, double* nn_ms, double* it_ms) {
   if (!c->timed[(c->n_iterates - 1) % icp_hip_ctx::kTimingRing])
     return fail(ICP_HIP_ENOTREADY, "the last iterate was not timed (config.timing_stride)");
   return icp_hip_timings(c, 1, nn_ms, it_ms);
+}
+
+int icp_hip_last_cull_path(icp_hip_ctx* c, int32_t* fused) {
+  if (!c || !fused) return fail(ICP_HIP_EINVAL, "null argument");
+  if (c->group) return group_cull_path(c, fused);
+  if (c->last_cull_path < 0) return fail(ICP_HIP_ENOTREADY, "no host-published iterate on this source");
+  *fused = c->last_cull_path;
+  return ICP_HIP_OK;
 }
 
 int icp_hip_comm_abort(icp_hip_ctx* c) {

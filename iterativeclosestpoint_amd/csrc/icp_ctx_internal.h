@@ -53,6 +53,8 @@ struct icp_hip_ctx {
   unsigned int last_lists[3] = {0, 0, 0};  // exact / ball / per-lane list sizes of the last search
   icp::Moments* mparts = nullptr;
   icp::CovMoments* cparts = nullptr;
+  icp::WaveStat* wstat = nullptr;  // the search's per-wave covariance records (wave_stats.h)
+  int last_cull_path = -1;         // IterDev::cull_mode of the last host-published iterate
   int64_t nb_mom = 0, nb_cull = 0;     // residual-moment parts, cull blocks
   bool lists_zero = true;               // fb_count is zero (reset by each iteration's publish)
   bool have_results = false;
@@ -119,6 +121,7 @@ int group_apply(icp_hip_ctx* c, const double* T);
 int group_get_source(icp_hip_ctx* c, double* xyz_out);
 int group_get_correspondences(icp_hip_ctx* c, int32_t* idx_out, double* dist_out);
 int group_traversal_counts(icp_hip_ctx* c, double* mean_entries, double* mean_points);
+int group_cull_path(icp_hip_ctx* c, int32_t* fused);
 int group_timings(icp_hip_ctx* c, int k, double* nn_ms, double* it_ms);
 int group_debug_counters(icp_hip_ctx* c, uint64_t out[ICP_DBG_SLOTS]);
 int group_synchronize(icp_hip_ctx* c);

@@ -339,6 +339,19 @@ int group_timings(icp_hip_ctx* c, int k, double* nn_ms, double* it_ms) {
   return ICP_HIP_OK;
 }
 
+int group_cull_path(icp_hip_ctx* c, int32_t* fused) {
+  // 1 only when every member's cull took its search's wave records
+  int32_t all = 1;
+  for (icp_hip_ctx* m : c->group->members) {
+    int32_t f = 0;
+    const int rc = icp_hip_last_cull_path(m, &f);
+    if (rc != ICP_HIP_OK) return rc;
+    all = all && f;
+  }
+  *fused = all;
+  return ICP_HIP_OK;
+}
+
 int group_debug_counters(icp_hip_ctx* c, uint64_t out[ICP_DBG_SLOTS]) {
   std::memset(out, 0, ICP_DBG_SLOTS * sizeof(uint64_t));
   for (icp_hip_ctx* m : c->group->members) {

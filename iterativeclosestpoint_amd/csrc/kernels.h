@@ -30,8 +30,28 @@ struct IterDev {
   CovMoments c_global;  // merged over ranks
   double mean, sd, thr, rmse;
   double cshift[6];  // this iteration's shift of the pair sums (set with the threshold)
+  // The band of the fused covariance sums (wave_stats.h), set at the end of every iterate for the
+  // next one's search: it sums the pairs with d <= fz_lo with the shift fz_sh and marks those in
+  // (fz_lo, fz_hi]. fz_ok = 0: no band (a new source, a non-finite threshold): full cull pass.
+  double fz_lo, fz_hi, fz_thr, fz_ok;
+  double fz_sh[6];
+  double cull_mode;  // this iterate: 1 = the search's wave records + the band pairs, 0 = full cull
+  double fz_pad;
   double pad[4];
 };
+
+// One wave's covariance record, written by the wave search's epilogue when the band is set
+// (wave_stats.h): the canonical sums of its pairs with d <= fz_lo (s: d^2, a - s, b - t, the 9
+// products), their count, the mask of its band lanes; flag = 1: the wave did not settle every
+// query itself (ball / exact / per-lane searches finish them): the cull kernel recomputes it.
+struct WaveStat {
+  double s[16];
+  double cnt;
+  unsigned long long bm;
+  unsigned long long flag;
+  double pad;
+};
+static_assert(sizeof(WaveStat) == 160, "WaveStat is 20 doubles");
 
 // The wave search's candidate cache (one record per wave of 64 queries): the box B+ whose leaves'
 // points were collected, their count and the generation (target / source upload) it belongs to.
@@ -90,6 +110,8 @@ struct NNLaunch {
   double wc_loose;          // a record is reused only while vol(B+) <= this x vol(B)
   double wc_lead;           // a stored B+ leads the wave's motion by this many iterates' displacement
   int certify_prev;         // previous-match certificate mode (icp_hip_config.certify_prev)
+  WaveStat* wstat;          // per-wave covariance records (null: none; the cull pass does it all)
+  const IterDev* fz;        // the band of this iterate (IterDev::fz_*)
 };
 
 // Threads per block of the per-thread search kernels for a given stack depth.
@@ -108,6 +130,8 @@ struct CullLaunch {
   const IterDev* it;
   CovMoments* part;
   int64_t n;
+  const double* dist;       // the residuals (the band's and the recomputed waves' pairs)
+  const WaveStat* wstat;    // the search's wave records (null: it wrote none this iterate)
 };
 
 // Residual moments of the settled queries in fixed parts (deterministic), then the merges.
@@ -146,9 +170,10 @@ struct IterPublish {
 
 
 int64_t cull_num_blocks(int64_t n);
-// 3-sigma cull + covariance part sums and their last merge level into it->c_local; with pub (no
-// communicator) also RMSE + publish. With a ticket counter and at most 4096 cull blocks the last
-// block runs the last level and the publish itself (one launch instead of two).
+// 3-sigma cull + covariance part sums (from the search's wave records and the band pairs, or a
+// full pass; wave_stats.h) and their last merge level into it->c_local; with pub (no
+// communicator) also RMSE + publish. With a ticket counter and a small grid the last block runs
+// the last level and the publish itself (one launch instead of two).
 hipError_t launch_cull_tail(const CullLaunch& a, unsigned* ticket, const IterPublish* pub, hipStream_t s);
 // Merge `nranks` gathered covariance moments in rank order, RMSE, publish.
 hipError_t launch_finalize_cov(const CovMoments* gathered, int nranks, IterDev* it, IterPublish pub, hipStream_t s);

@@ -23,6 +23,7 @@
 
 #include "kernels.h"
 #include "nn_device.h"
+#include "wave_stats.h"
 
 // Diagnostic build only (-DICP_PHASE_CLOCKS=1): per-phase s_memtime deltas of the wave search
 // summed into the debug slots 16..21 (the product build has no clock reads).
@@ -175,6 +176,54 @@ __device__ __forceinline__ unsigned xcd_block(unsigned chunk) {
   return ((k / chunk) * 8u + x) * chunk + k % chunk;
 }
 
+// The wave's covariance record (wave_stats.h), once the wave has settled its queries: the
+// canonical sums of its pairs below the band, its band lanes, or flag = 1 when some of its queries
+// are left to the other searches (the cull kernel then recomputes the whole wave, so the sums are
+// the same whichever path settled which query). Every lane calls it (wave-uniform exits).
+template <bool DBG>
+__device__ __forceinline__ void wave_record(const NNLaunch& a, uint32_t wid, int lane, bool active, bool settled,
+                                            double d, int32_t pos, double qx, double qy, double qz,
+                                            unsigned char* wl) {
+  if (a.wstat == nullptr || !(a.fz->fz_ok != 0.0)) return;
+  WaveStat* rec = a.wstat + wid;
+  if (__ballot(active && !settled) != 0) {
+    if (lane == 0) {
+      rec->flag = 1ull;
+      if (DBG && kDbgCounts && a.dbg) atomicAdd(&a.dbg[30], 1ull);
+    }
+    return;
+  }
+  const double lo = a.fz->fz_lo, hi = a.fz->fz_hi;
+  const bool in = active && d <= lo;
+  const bool band = active && !(d <= lo) && d <= hi;
+  double mx = 0.0, my = 0.0, mz = 0.0;
+  if (in) {
+    const TgtPt* p = a.pts + pos;
+    const double2 xy = *reinterpret_cast<const double2*>(&p->x);
+    mx = xy.x;
+    my = xy.y;
+    mz = p->z;
+  }
+  double sh[6];
+#pragma unroll
+  for (int k = 0; k < 6; k++) sh[k] = a.fz->fz_sh[k];
+  wave_lds_fence();  // the scan's reads of the staging area are done
+  double r1, r2;
+  wave_cov_sums(in, d, qx, qy, qz, mx, my, mz, sh, reinterpret_cast<double*>(wl), lane, r1, r2);
+  const unsigned long long am = __ballot(in), bm = __ballot(band);
+  if ((lane & 7) == 0) {
+    rec->s[lane >> 3] = r1;
+    rec->s[8 + (lane >> 3)] = r2;
+  }
+  if (lane == 0) {
+    rec->cnt = (double)__popcll(am);
+    rec->bm = bm;
+    rec->flag = 0ull;
+    if (DBG && kDbgCounts && a.dbg) atomicAdd(&a.dbg[31], (unsigned long long)__popcll(bm));
+  }
+}
+static_assert(kStatLds <= kWaveLds, "the record's reduction fits the wave's LDS area");
+
 // The search of one wave's queries (query i per lane; i >= n: an idle lane). HALF: the second
 // pass over the 32-query halves of the waves whose box overflowed (k_nn_half: queries already
 // moved, no candidate cache; lanes 32..63 idle).
@@ -313,14 +362,22 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
     }
     if (open == 0 || (a.certify_prev == 3 && __popcll(open) <= kOpenToBall)) {
       store_query32<APPLY>(a, i, active, qx, qy, qz);
-      if (safe) qat(a.dist_out, i) = __builtin_sqrt(u);
+      double d = 0.0;
+      int32_t pos = prev_pos;
+      if (safe) {
+        d = __builtin_sqrt(u);
+        qat(a.dist_out, i) = d;
+      }
       if (open != 0) {
         if (active && !finite_q) {
-          qat(a.pos_out, i) = a.pos0;
-          qat(a.dist_out, i) = residual_to(a.pts, a.pos0, qx, qy, qz);
+          pos = a.pos0;
+          d = residual_to(a.pts, a.pos0, qx, qy, qz);
+          qat(a.pos_out, i) = pos;
+          qat(a.dist_out, i) = d;
         }
         wave_append_u(active && finite_q && !safe, i, u, a.fb_count + 1, a.fb_list2, a.fb_u2);
       }
+      if (!HALF) wave_record<DBG>(a, wid, lane, active, safe || !finite_q, d, pos, qx, qy, qz, wl);
       return;
     }
     if (a.certify_prev == 1) safe = false;  // the whole wave searches
@@ -1075,6 +1132,9 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
   wave_append(to_exact, i, a.fb_count, a.fb_list);
   const bool covered = !(join && !(best <= u));
   wave_append_u(to_lane, i, covered ? u : __builtin_inf(), a.fb_count + 1, a.fb_list2, a.fb_u2);
+  if (!HALF)
+    wave_record<DBG>(a, wid, lane, active, safe || written, safe ? __builtin_sqrt(u) : d, safe ? prev_pos : pos, qx,
+                     qy, qz, wl);
 #if ICP_PHASE_CLOCKS
   PCLK(t_p5);
   if (a.dbg && lane == 0) {

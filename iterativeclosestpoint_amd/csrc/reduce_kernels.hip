@@ -1,8 +1,9 @@
 // reduce_kernels.hip — gfx950 reductions of one ICP iteration after the correspondence search.
 //
 //  k_moments        residual moments of fixed 4096-query parts (icpengine.cpp:235-245)
-//  k_cull_cov       3-sigma cull (icpengine.cpp:263-278) + valid-pair centroid and cross-covariance
-//                   sums (icpengine.cpp:76-90, computeBestFitTransform's H = AA * BB^T)
+//  k_cull_waves     3-sigma cull (icpengine.cpp:263-278) + valid-pair centroid and cross-covariance
+//                   sums (icpengine.cpp:76-90, computeBestFitTransform's H = AA * BB^T), from the
+//                   wave search's per-wave records and the band pairs (wave_stats.h), or in full
 //  k_tree_merge, k_merge_*_last   fixed-shape merge trees of the part sums (deterministic)
 //  k_finalize_*     rank-ordered merge of the gathered per-rank records (multi-GPU)
 //  publish          the last kernel of an iteration stores the finished record into pinned host
@@ -15,6 +16,7 @@
 
 #include "kernels.h"
 #include "nn_device.h"
+#include "wave_stats.h"
 
 namespace icp {
 
@@ -133,7 +135,7 @@ constexpr int kLastSpan = 4096;
 // t + s's value into its own. Steps 1..32 run inside each wave through shuffles, steps 64 and 128
 // over the four wave results: the same merges in the same order as the tree in LDS this replaced
 // (bit-identical), with 4 entries of LDS instead of 256 (so the cull blocks can run the last level
-// themselves, k_cull_cov's fused tail).
+// themselves, k_cull_waves' fused tail).
 template <typename T>
 __device__ __forceinline__ T shfl_down_T(const T& v, int s) {
   static_assert(sizeof(T) % sizeof(double) == 0, "records of doubles");
@@ -263,6 +265,42 @@ __device__ void finalize_moments(IterDev* it, const Moments& g, const MomentsFin
   it->thr = cull_threshold(mean, sd, f.k_sigma, f.iter, f.engine_rules);
 }
 
+// With the threshold known (every thread of the first wave calls it): the shift of the pair sums
+// and the cull's mode. A band set by the previous iterate fixes the shift (the search summed with
+// it); the wave records count when the search wrote them and the threshold lies inside the band.
+__device__ void cull_params(IterDev* it, double thr, const CullLaunch& cl) {
+  const bool fz = it->fz_ok != 0.0;
+  if (fz) {
+    if (threadIdx.x < 6) it->cshift[threadIdx.x] = it->fz_sh[threadIdx.x];
+  } else {
+    cov_shift_store(cl.x, cl.y, cl.z, cl.pos, cl.pts, cl.n, thr, it);
+  }
+  if (threadIdx.x == 0)
+    it->cull_mode = (fz && cl.wstat != nullptr && it->fz_lo <= thr && thr <= it->fz_hi) ? 1.0 : 0.0;
+}
+
+// The band of the next iterate's search (thread 0, once the iterate is finished): around this
+// threshold, as wide as twice its last relative change plus 5 % (at most 50 %; 25 % after a new
+// source), with this iterate's pair shift.
+__device__ void band_next(IterDev* it) {
+  const double thr = it->thr;
+  double delta = 0.25;
+  if (it->fz_ok != 0.0 && it->fz_thr > 0.0) {
+    const double r = thr / it->fz_thr - 1.0;
+    delta = 2.0 * __builtin_fabs(r) + 0.05;
+    delta = delta < 0.5 ? delta : 0.5;
+  }
+  bool fin = __builtin_isfinite(thr) && thr > 0.0 && delta == delta;
+  for (int k = 0; k < 6; k++) {
+    fin = fin && __builtin_isfinite(it->cshift[k]);
+    it->fz_sh[k] = it->cshift[k];
+  }
+  it->fz_lo = thr * (1.0 - delta);
+  it->fz_hi = thr * (1.0 + delta);
+  it->fz_thr = thr;
+  it->fz_ok = fin ? 1.0 : 0.0;
+}
+
 // The last level of the residual moments: the merged part sums -> (count, mean, M2) in
 // it->m_local; with finalize (one rank, no communicator) also mean/std/threshold and the cull's
 // pair shift. Run by k_merge_moments_last or by k_moments' last block (identical bits: the same
@@ -295,8 +333,8 @@ __device__ void moments_last(const MomSums& r, double c, const MomTail& t) {
   }
   if (!t.finalize) return;
   __syncthreads();
-  // the threshold, then the pair shift of the cull (the first wave)
-  cov_shift_store(t.cl.x, t.cl.y, t.cl.z, t.cl.pos, t.cl.pts, t.cl.n, thr_s, t.it);
+  // the threshold, then the pair shift and the mode of the cull (the first wave)
+  if (threadIdx.x < 64) cull_params(t.it, thr_s, t.cl);
 }
 
 template <bool FUSE>
@@ -373,7 +411,7 @@ __global__ void __launch_bounds__(64) k_finalize_moments(const Moments* gathered
     thr_s = it->thr;
   }
   __syncthreads();
-  cov_shift_store(cl.x, cl.y, cl.z, cl.pos, cl.pts, cl.n, thr_s, it);
+  cull_params(it, thr_s, cl);
 }
 
 // The device loop's step (one thread): the session's decisions on this iteration's finished
@@ -439,6 +477,7 @@ __device__ void finalize_cov_publish(IterDev* it, const CovMoments& g, IterPubli
     for (int k = 0; k < 5; k++) pub.lists[k] = 0u;  // + the half list of the wave search
     it->c_global = rec->c_global;
     it->rmse = rec->rmse;
+    band_next(it);
     if (LOOP && pub.loop) loop_step(pub.loop, *rec, pub.rec);
   }
   if (LOOP && pub.loop) return;  // the device loop: the host reads the batch's records after it
@@ -452,9 +491,9 @@ __device__ void finalize_cov_publish(IterDev* it, const CovMoments& g, IterPubli
 }
 
 // The last level of the covariance sums: the merged part sums -> it->c_local; with finalize (one
-// rank) also RMSE and the publish. Run by k_merge_cov_last or by k_cull_cov's last block.
+// rank) also RMSE and the publish. Run by k_merge_cov_last or by k_cull_waves' last block.
 struct CovTail {
-  unsigned* ticket;  // non-null: k_cull_cov's last block runs the last level (<= kLastSpan blocks)
+  unsigned* ticket;  // non-null: k_cull_waves' last block runs the last level (<= kLastSpan blocks)
   IterPublish pub;
   int finalize;
 };
@@ -499,89 +538,148 @@ __global__ void __launch_bounds__(64) k_finalize_cov(const CovMoments* gathered,
   finalize_cov_publish(it, g, pub, &rec);
 }
 
-// 3-sigma cull + covariance sums. One thread per 4 queries (1024 per block). A thread first
-// issues all its streamed loads (pos, x, y, z of its 4 queries), then all 4 match gathers, then
-// accumulates in query order: two dependent memory round trips. The residual is not read: every
-// search path stores d = sqrt(fl(dx^2 + dy^2 + dz^2)) of the query and its match (nn_device.h,
-// octree.cpp:139-144 arithmetic; a non-finite query's default match included), so the same
-// operations on the same operands give its bits again (8 of 68 B per query not streamed).
-constexpr int kCullPer = 4;
+// 3-sigma cull + covariance sums of kCullWaves search waves (64 queries each) per block:
+//   1. a wave record written by the search (cull_mode 1, flag 0) is taken as it is;
+//   2. the other waves are recomputed here by one wave each with the search's own function
+//      (wave_stats.h wave_cov_sums): against the band's lower end in mode 1, against the
+//      threshold itself in mode 0 (no records, or the threshold left the band);
+//   3. each wave's band pairs (mode 1) with d <= thr are added in lane order;
+//   4. the block's fixed pairwise tree over its waves.
+// So a wave's sums do not depend on which search settled which of its queries, nor on which
+// block recomputed it. The residual is read, not recomputed: every search path stores
+// d = sqrt(fl(dx^2 + dy^2 + dz^2)) (octree.cpp:139-144), and the pairs' terms use it as it is.
+constexpr int kCullWaves = 64;
 
 // FUSE: the last block runs the last merge level and (finalize) the publish; not with the device
 // loop (whose step would put the SVD's registers into every cull block): that one keeps
 // k_merge_cov_last.
 template <bool FUSE>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k_cull_cov(CullLaunch a, CovTail tail) {
+__global__ void __launch_bounds__(256) k_cull_waves(CullLaunch a, CovTail tail) {
   if (a.loop && a.loop->core.done) return;  // the device loop's session finished (block-uniform)
-  __shared__ double red[4 * 17];
-  const double thr = a.it->thr;
+  __shared__ double red[4][64 * kStatStride];
+  __shared__ double slot[kCullWaves][18];  // the wave's 16 sums, its count, its band mask (bits)
+  __shared__ int list[kCullWaves];
+  __shared__ int nlist;
+  const IterDev* it = a.it;
+  const double thr = it->thr;
+  const bool fused = it->cull_mode != 0.0;
+  const double lo = it->fz_lo, hi = it->fz_hi;
   double sh[6];
 #pragma unroll
-  for (int k = 0; k < 6; k++) sh[k] = a.it->cshift[k];
-  const int64_t base = (int64_t)blockIdx.x * (256 * kCullPer) + threadIdx.x;
-  // count, sum d^2, sum (a - s), sum (b - t), sum (a - s)(b - t)^T over the valid pairs
-  double v[17];
+  for (int k = 0; k < 6; k++) sh[k] = it->cshift[k];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int64_t nwaves = (a.n + 63) / 64;
+  const int64_t w0 = (int64_t)blockIdx.x * kCullWaves;
+  if (t == 0) nlist = 0;
+  __syncthreads();
+  if (t < kCullWaves) {
+    const int64_t w = w0 + t;
+    bool need = false;
+    if (w < nwaves) {
+      if (fused) {
+        const WaveStat* r = a.wstat + w;
+        if (r->flag != 0ull) {
+          need = true;
+        } else {
 #pragma unroll
-  for (int k = 0; k < 17; k++) v[k] = 0.0;
-  double qx[kCullPer], qy[kCullPer], qz[kCullPer];
-  int32_t pq[kCullPer];
-#pragma unroll
-  for (int e = 0; e < kCullPer; e++) {
-    const int64_t i = base + e * 256;
-    const bool in = i < a.n;
-    pq[e] = in ? a.pos[i] : 0;
-    qx[e] = in ? a.x[i] : 0.0;
-    qy[e] = in ? a.y[i] : 0.0;
-    qz[e] = in ? a.z[i] : 0.0;
-  }
-  double mx[kCullPer], my[kCullPer], mz[kCullPer];
-#pragma unroll
-  for (int e = 0; e < kCullPer; e++) {
-    const TgtPt* p = a.pts + pq[e];
-    const double2 pxy = *reinterpret_cast<const double2*>(&p->x);
-    mx[e] = pxy.x;
-    my[e] = pxy.y;
-    mz[e] = p->z;
-  }
-#pragma unroll
-  for (int e = 0; e < kCullPer; e++) {
-    const double ex = mx[e] - qx[e], ey = my[e] - qy[e], ez = mz[e] - qz[e];
-    // the stored residual, bit for bit (NaN past the end: NaN <= thr is false)
-    const double d = base + e * 256 < a.n ? __builtin_sqrt(ex * ex + ey * ey + ez * ez) : __builtin_nan("");
-    if (d <= thr) {  // icpengine.cpp:265
-      const double da[3] = {qx[e] - sh[0], qy[e] - sh[1], qz[e] - sh[2]};
-      const double db[3] = {mx[e] - sh[3], my[e] - sh[4], mz[e] - sh[5]};
-      v[0] += 1.0;
-      v[1] += d * d;
-#pragma unroll
-      for (int r = 0; r < 3; r++) {
-        v[2 + r] += da[r];
-        v[5 + r] += db[r];
-#pragma unroll
-        for (int c = 0; c < 3; c++) v[8 + 3 * r + c] += da[r] * db[c];
+          for (int k = 0; k < 16; k++) slot[t][k] = r->s[k];
+          slot[t][16] = r->cnt;
+          slot[t][17] = __longlong_as_double((long long)r->bm);
+        }
+      } else {
+        need = true;
       }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 18; k++) slot[t][k] = 0.0;
+    }
+    if (need) list[atomicAdd(&nlist, 1)] = t;  // any order: each entry is one wave's own slot
+  }
+  __syncthreads();
+  const int nl = nlist;
+  // software-pipelined: the next wave's residual, query and position are loaded while this
+  // one's match is gathered and summed (one dependent round trip per wave instead of three)
+  double cd = 0.0, cx = 0.0, cy = 0.0, cz = 0.0;
+  int32_t cp = 0;
+  auto load = [&](int e) {
+    const int64_t i = (w0 + list[e]) * 64 + lane;
+    const bool act = i < a.n;
+    cd = act ? a.dist[i] : 0.0;
+    cx = act ? a.x[i] : 0.0;
+    cy = act ? a.y[i] : 0.0;
+    cz = act ? a.z[i] : 0.0;
+    cp = act ? a.pos[i] : 0;
+  };
+  if (wv < nl) load(wv);
+  for (int e = wv; e < nl; e += 4) {
+    const int tt = list[e];
+    const int64_t i = (w0 + tt) * 64 + lane;
+    const bool active = i < a.n;
+    const double d = cd, qx = cx, qy = cy, qz = cz;
+    const int32_t ps = cp;
+    const bool in = active && (fused ? d <= lo : d <= thr);
+    const bool band = fused && active && !(d <= lo) && d <= hi;
+    double mx = 0.0, my = 0.0, mz = 0.0;
+    if (in) {
+      const TgtPt* p = a.pts + ps;
+      const double2 xy = *reinterpret_cast<const double2*>(&p->x);
+      mx = xy.x;
+      my = xy.y;
+      mz = p->z;
+    }
+    if (e + 4 < nl) load(e + 4);
+    double r1, r2;
+    wave_cov_sums(in, d, qx, qy, qz, mx, my, mz, sh, red[wv], lane, r1, r2);
+    const unsigned long long am = __ballot(in), bm = __ballot(band);
+    if ((lane & 7) == 0) {
+      slot[tt][lane >> 3] = r1;
+      slot[tt][8 + (lane >> 3)] = r2;
+    }
+    if (lane == 0) {
+      slot[tt][16] = (double)__popcll(am);
+      slot[tt][17] = __longlong_as_double((long long)bm);
     }
   }
-  block_sum<17>(v, red);
-  CovSums m;
-  m.n = v[0];
-  m.sum_d2 = v[1];
-  for (int k = 0; k < 3; k++) {
-    m.sa[k] = v[2 + k];
-    m.sb[k] = v[5 + k];
-    m.pad[k] = 0.0;
+  __syncthreads();
+  CovSums m = covsum_identity();
+  if (t < kCullWaves && w0 + t < nwaves) {
+    double s[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) s[k] = slot[t][k];
+    double cnt = slot[t][16];
+    unsigned long long bm = (unsigned long long)__double_as_longlong(slot[t][17]);
+    const int64_t base = (w0 + t) * 64;
+    while (bm) {  // the band pairs below the threshold, in lane order
+      const int l = __builtin_ctzll(bm);
+      bm &= bm - 1ull;
+      const int64_t i = base + l;
+      const double d = a.dist[i];
+      if (d <= thr) {  // icpengine.cpp:265
+        const TgtPt* p = a.pts + a.pos[i];
+        add_pair(s, cnt, d, a.x[i], a.y[i], a.z[i], p->x, p->y, p->z, sh);
+      }
+    }
+    m.n = cnt;
+    m.sum_d2 = s[0];
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      m.sa[k] = s[1 + k];
+      m.sb[k] = s[4 + k];
+    }
+#pragma unroll
+    for (int k = 0; k < 9; k++) m.sab[k] = s[7 + k];
   }
-  for (int k = 0; k < 9; k++) m.sab[k] = v[8 + k];
+  __shared__ CovSums sm[4];
+  const CovSums r = block_tree<CovSums, covsum_merge, covsum_identity>(m, sm);
   CovSums* part = reinterpret_cast<CovSums*>(a.part);
   if (!FUSE) {
-    if (threadIdx.x == 0) part[blockIdx.x] = m;
+    if (t == 0) part[blockIdx.x] = r;
     return;
   }
   __shared__ int last_s;
-  if (!publish_part_last(part, m, tail.ticket, &last_s)) return;
-  __shared__ CovSums sm[4];
-  const CovSums r = block_tree_last_sc1<CovSums, covsum_merge, covsum_identity>(part, gridDim.x, sm);
-  cov_last<false>(r, a.it, const_cast<IterDev*>(a.it), tail);
+  if (!publish_part_last(part, r, tail.ticket, &last_s)) return;
+  const CovSums rr = block_tree_last_sc1<CovSums, covsum_merge, covsum_identity>(part, gridDim.x, sm);
+  cov_last<false>(rr, a.it, const_cast<IterDev*>(a.it), tail);
 }
 
 template <typename T, T (*Merge)(const T&, const T&), T (*Identity)()>
@@ -637,17 +735,17 @@ hipError_t launch_finalize_moments(const Moments* gathered, int nranks, IterDev*
   return hipGetLastError();
 }
 
-int64_t cull_num_blocks(int64_t n) { return (n + 256 * kCullPer - 1) / (256 * kCullPer); }
+int64_t cull_num_blocks(int64_t n) { return ((n + 63) / 64 + kCullWaves - 1) / kCullWaves; }
 
 hipError_t launch_cull_tail(const CullLaunch& a, unsigned* ticket, const IterPublish* pub, hipStream_t s) {
   const int64_t nb = cull_num_blocks(a.n);
   CovTail tail{nullptr, pub ? *pub : IterPublish{nullptr, nullptr, 0.0, nullptr, nullptr}, pub ? 1 : 0};
   if (ticket && nb >= 1 && nb <= kFuseMaxBlocks && !a.loop) {  // one launch: the last block merges and publishes
     tail.ticket = ticket;
-    hipLaunchKernelGGL(k_cull_cov<true>, dim3((unsigned)nb), dim3(256), 0, s, a, tail);
+    hipLaunchKernelGGL(k_cull_waves<true>, dim3((unsigned)nb), dim3(256), 0, s, a, tail);
     return hipGetLastError();
   }
-  if (a.n > 0) hipLaunchKernelGGL(k_cull_cov<false>, dim3((unsigned)nb), dim3(256), 0, s, a, tail);
+  if (a.n > 0) hipLaunchKernelGGL(k_cull_waves<false>, dim3((unsigned)nb), dim3(256), 0, s, a, tail);
   int64_t np = nb;
   const CovSums* cur = merge_to_last_span<CovSums, covsum_merge, covsum_identity>(
       reinterpret_cast<const CovSums*>(a.part), &np, s);
