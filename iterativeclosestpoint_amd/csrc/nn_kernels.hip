@@ -208,13 +208,9 @@ __device__ __forceinline__ void wave_record(const NNLaunch& a, uint32_t wid, int
 #pragma unroll
   for (int k = 0; k < 6; k++) sh[k] = a.fz->fz_sh[k];
   wave_lds_fence();  // the scan's reads of the staging area are done
-  double r1, r2;
-  wave_cov_sums(in, d, qx, qy, qz, mx, my, mz, sh, reinterpret_cast<double*>(wl), lane, r1, r2);
+  const double r = wave_cov_sums(in, d, qx, qy, qz, mx, my, mz, sh, reinterpret_cast<double*>(wl), lane);
   const unsigned long long am = __ballot(in), bm = __ballot(band);
-  if ((lane & 7) == 0) {
-    rec->s[lane >> 3] = r1;
-    rec->s[8 + (lane >> 3)] = r2;
-  }
+  if (lane < 16) rec->s[lane] = r;
   if (lane == 0) {
     rec->cnt = (double)__popcll(am);
     rec->bm = bm;

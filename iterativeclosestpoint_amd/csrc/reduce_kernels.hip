@@ -215,15 +215,14 @@ __device__ __forceinline__ T block_tree_last_sc1(const T* in, int64_t n, T* sm) 
 // block: speed only) with a top counter that the last arrival of each shard bumps: arrivals on
 // one device-scope counter serialise at ~12 ns each (microarch guide, fanin), which cost 15 us
 // for the 1221 cull blocks of a 1.25M shard with a single counter.
-// Fused only for small grids: every block then pays a store wait and a returned atomic before it
-// retires, and the fused cull instance holds the last level's registers (128 VGPRs: 4 waves per
-// SIMD instead of 5). Measured (one MI355X, interleaved): 100k queries (25 moment parts, 98 cull
-// blocks) -2 us per iteration; at 1221 cull blocks (a 1.25M shard) +15 us, at 2442 moment parts
-// (10M) +40 us with the registers of the device loop's step in the fused cull (since removed).
-constexpr int kFuseMaxBlocks = 256;
-// the moments blocks are short and register-light: fused up to 512 parts (2M queries; at 2442
-// parts, 10M, the per-block ticket cost 5 us more than the separate launch)
+// Fused only for moderate grids: every block then pays a store wait and a returned atomic before
+// it retires. Measured (one MI355X, interleaved, r18 with the former 1024-query cull blocks):
+// 100k queries (25 moment parts, 98 cull blocks) -2 us per iteration; at 1221 cull blocks (a
+// 1.25M shard) +15 us, at 2442 moment parts (10M) +5 us.
+// the moments blocks: fused up to 512 parts (2M queries)
 constexpr int kFuseMaxMomentParts = 512;
+// the cull blocks (256 search waves each: 611 at 10M) up to 1024 blocks (16.7M queries)
+constexpr int kFuseMaxCullBlocks = 1024;
 constexpr int kTicketLine = 32;                      // uints per counter line (128 B)
 constexpr int kTicketWords = 9 * kTicketLine;        // top + 8 shards
 template <typename T>
@@ -524,9 +523,15 @@ __device__ void cov_last(const CovSums& r, const IterDev* shift_src, IterDev* it
   finalize_cov_publish<LOOP>(it, res, t.pub, &rec);
 }
 
+template <bool SC1>
+__device__ CovSums fold_parts(const CovSums* in, int64_t n, double (*rows)[20], double* gsum);
+
+// The last level of the cull's part sums as its own launch (the device loop; more than
+// kFuseMaxCullBlocks blocks): fold_parts, the order of the fused last block.
 __global__ void __launch_bounds__(256) k_merge_cov_last(const CovSums* in, int64_t n, IterDev* it, CovTail tail) {
-  __shared__ CovSums sm[4];
-  const CovSums r = block_tree_last<CovSums, covsum_merge, covsum_identity>(in, n, sm);
+  __shared__ __attribute__((aligned(16))) double rows[256][20];
+  __shared__ double gsum[8 * 17];
+  const CovSums r = fold_parts<false>(in, n, rows, gsum);
   cov_last<true>(r, it, it, tail);
 }
 
@@ -539,16 +544,81 @@ __global__ void __launch_bounds__(64) k_finalize_cov(const CovMoments* gathered,
 }
 
 // 3-sigma cull + covariance sums of kCullWaves search waves (64 queries each) per block:
-//   1. a wave record written by the search (cull_mode 1, flag 0) is taken as it is;
-//   2. the other waves are recomputed here by one wave each with the search's own function
-//      (wave_stats.h wave_cov_sums): against the band's lower end in mode 1, against the
-//      threshold itself in mode 0 (no records, or the threshold left the band);
+//   1. the block's wave records (written by the search, cull_mode 1) are copied to LDS, coalesced;
+//   2. the waves without one (flag 1; every wave in mode 0) are recomputed by one wave each with
+//      the search's own function (wave_stats.h wave_cov_sums): against the band's lower end in
+//      mode 1, against the threshold itself in mode 0 (no records, or the threshold left the band);
 //   3. each wave's band pairs (mode 1) with d <= thr are added in lane order;
-//   4. the block's fixed pairwise tree over its waves.
+//   4. the block's column fold over its waves (fold_rows).
 // So a wave's sums do not depend on which search settled which of its queries, nor on which
 // block recomputed it. The residual is read, not recomputed: every search path stores
 // d = sqrt(fl(dx^2 + dy^2 + dz^2)) (octree.cpp:139-144), and the pairs' terms use it as it is.
-constexpr int kCullWaves = 64;
+constexpr int kCullWaves = 256;  // search waves per block: one record row per thread
+constexpr int kRow = 20;         // doubles per row: the WaveStat layout (s[16], cnt, bm, flag, pad)
+static_assert(sizeof(WaveStat) == kRow * sizeof(double), "rows are wave records");
+
+// Column v of the 17 summed values in CovSums order (n, sum d^2, sa[3], sb[3], sab[9]) -> its
+// index in a row.
+__device__ __forceinline__ int row_col(int v) { return v == 0 ? 16 : v - 1; }
+
+// The fixed-order column sums of 256 rows (LDS): thread 17 g + v (g < 8) adds column v of rows
+// 32 g .. 32 g + 31 in order, then thread v adds the 8 group sums in order. Every thread of the
+// (256-thread) block calls it; the result is the same for all.
+__device__ CovSums fold_rows(const double (*rows)[kRow], double* gsum) {
+  const int t = threadIdx.x;
+  if (t < 8 * 17) {
+    const int g = t / 17, v = t % 17, c = row_col(v);
+    double acc = rows[32 * g][c];
+#pragma unroll 8
+    for (int i = 1; i < 32; i++) acc += rows[32 * g + i][c];
+    gsum[g * 17 + v] = acc;
+  }
+  __syncthreads();
+  __shared__ double col[17];
+  if (t < 17) {
+    double acc = gsum[t];
+#pragma unroll
+    for (int g = 1; g < 8; g++) acc += gsum[g * 17 + t];
+    col[t] = acc;
+  }
+  __syncthreads();
+  CovSums r;
+  r.n = col[0];
+  r.sum_d2 = col[1];
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    r.sa[k] = col[2 + k];
+    r.sb[k] = col[5 + k];
+    r.pad[k] = 0.0;
+  }
+#pragma unroll
+  for (int k = 0; k < 9; k++) r.sab[k] = col[8 + k];
+  __syncthreads();
+  return r;
+}
+
+// The last level over n <= 4096 part sums (the cull blocks'), the same in k_cull_waves' last
+// block (SC1: parts other blocks of the launch stored with sc1 stores) and in k_merge_cov_last
+// (the device loop's path): thread t adds parts t + 256 k in order into its row, then fold_rows.
+template <bool SC1>
+__device__ CovSums fold_parts(const CovSums* in, int64_t n, double (*rows)[kRow], double* gsum) {
+  const int t = threadIdx.x;
+  double acc[17];
+#pragma unroll
+  for (int v = 0; v < 17; v++) acc[v] = 0.0;
+  for (int k = 0; k < 16; k++) {
+    const int64_t g = (int64_t)t + 256 * k;
+    if (g >= n) break;
+    const CovSums c = SC1 ? load_sc1(in + g) : in[g];
+    const double* cw = reinterpret_cast<const double*>(&c);
+#pragma unroll
+    for (int v = 0; v < 17; v++) acc[v] = k == 0 ? cw[v] : acc[v] + cw[v];
+  }
+#pragma unroll
+  for (int v = 0; v < 17; v++) rows[t][row_col(v)] = acc[v];
+  __syncthreads();
+  return fold_rows(rows, gsum);
+}
 
 // FUSE: the last block runs the last merge level and (finalize) the publish; not with the device
 // loop (whose step would put the SVD's registers into every cull block): that one keeps
@@ -556,8 +626,9 @@ constexpr int kCullWaves = 64;
 template <bool FUSE>
 __global__ void __launch_bounds__(256) k_cull_waves(CullLaunch a, CovTail tail) {
   if (a.loop && a.loop->core.done) return;  // the device loop's session finished (block-uniform)
-  __shared__ double red[4][64 * kStatStride];
-  __shared__ double slot[kCullWaves][18];  // the wave's 16 sums, its count, its band mask (bits)
+  __shared__ __attribute__((aligned(16))) double rows[kCullWaves][kRow];
+  __shared__ __attribute__((aligned(32))) double red[4][kStatLds / 8];
+  __shared__ double gsum[8 * 17];
   __shared__ int list[kCullWaves];
   __shared__ int nlist;
   const IterDev* it = a.it;
@@ -570,30 +641,22 @@ __global__ void __launch_bounds__(256) k_cull_waves(CullLaunch a, CovTail tail) 
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int64_t nwaves = (a.n + 63) / 64;
   const int64_t w0 = (int64_t)blockIdx.x * kCullWaves;
+  const int nw = (int)(nwaves - w0 < kCullWaves ? nwaves - w0 : kCullWaves);  // this block's waves
   if (t == 0) nlist = 0;
+  if (fused) {
+    // the block's records, 16-B loads over the whole block (coalesced)
+    const double2* src = reinterpret_cast<const double2*>(a.wstat + w0);
+    double2* dst = reinterpret_cast<double2*>(&rows[0][0]);
+    for (int k = t; k < nw * (kRow / 2); k += 256) dst[k] = src[k];
+  }
   __syncthreads();
   if (t < kCullWaves) {
-    const int64_t w = w0 + t;
-    bool need = false;
-    if (w < nwaves) {
-      if (fused) {
-        const WaveStat* r = a.wstat + w;
-        if (r->flag != 0ull) {
-          need = true;
-        } else {
+    const bool need = t < nw && (!fused || reinterpret_cast<const unsigned long long*>(rows[t])[18] != 0ull);
+    if (t >= nw) {
 #pragma unroll
-          for (int k = 0; k < 16; k++) slot[t][k] = r->s[k];
-          slot[t][16] = r->cnt;
-          slot[t][17] = __longlong_as_double((long long)r->bm);
-        }
-      } else {
-        need = true;
-      }
-    } else {
-#pragma unroll
-      for (int k = 0; k < 18; k++) slot[t][k] = 0.0;
+      for (int k = 0; k < kRow; k++) rows[t][k] = 0.0;
     }
-    if (need) list[atomicAdd(&nlist, 1)] = t;  // any order: each entry is one wave's own slot
+    if (need) list[atomicAdd(&nlist, 1)] = t;  // any order: each entry is one wave's own row
   }
   __syncthreads();
   const int nl = nlist;
@@ -628,49 +691,40 @@ __global__ void __launch_bounds__(256) k_cull_waves(CullLaunch a, CovTail tail) 
       mz = p->z;
     }
     if (e + 4 < nl) load(e + 4);
-    double r1, r2;
-    wave_cov_sums(in, d, qx, qy, qz, mx, my, mz, sh, red[wv], lane, r1, r2);
+    const double r = wave_cov_sums(in, d, qx, qy, qz, mx, my, mz, sh, red[wv], lane);
     const unsigned long long am = __ballot(in), bm = __ballot(band);
-    if ((lane & 7) == 0) {
-      slot[tt][lane >> 3] = r1;
-      slot[tt][8 + (lane >> 3)] = r2;
-    }
+    if (lane < 16) rows[tt][lane] = r;
     if (lane == 0) {
-      slot[tt][16] = (double)__popcll(am);
-      slot[tt][17] = __longlong_as_double((long long)bm);
+      rows[tt][16] = (double)__popcll(am);
+      reinterpret_cast<unsigned long long*>(rows[tt])[17] = bm;
     }
   }
   __syncthreads();
-  CovSums m = covsum_identity();
-  if (t < kCullWaves && w0 + t < nwaves) {
-    double s[16];
+  if (t < nw) {
+    unsigned long long bm = reinterpret_cast<const unsigned long long*>(rows[t])[17];
+    if (fused && bm) {
+      double s[16];
 #pragma unroll
-    for (int k = 0; k < 16; k++) s[k] = slot[t][k];
-    double cnt = slot[t][16];
-    unsigned long long bm = (unsigned long long)__double_as_longlong(slot[t][17]);
-    const int64_t base = (w0 + t) * 64;
-    while (bm) {  // the band pairs below the threshold, in lane order
-      const int l = __builtin_ctzll(bm);
-      bm &= bm - 1ull;
-      const int64_t i = base + l;
-      const double d = a.dist[i];
-      if (d <= thr) {  // icpengine.cpp:265
-        const TgtPt* p = a.pts + a.pos[i];
-        add_pair(s, cnt, d, a.x[i], a.y[i], a.z[i], p->x, p->y, p->z, sh);
+      for (int k = 0; k < 16; k++) s[k] = rows[t][k];
+      double cnt = rows[t][16];
+      const int64_t base = (w0 + t) * 64;
+      while (bm) {  // the band pairs below the threshold, in lane order
+        const int l = __builtin_ctzll(bm);
+        bm &= bm - 1ull;
+        const int64_t i = base + l;
+        const double d = a.dist[i];
+        if (d <= thr) {  // icpengine.cpp:265
+          const TgtPt* p = a.pts + a.pos[i];
+          add_pair(s, cnt, d, a.x[i], a.y[i], a.z[i], p->x, p->y, p->z, sh);
+        }
       }
-    }
-    m.n = cnt;
-    m.sum_d2 = s[0];
 #pragma unroll
-    for (int k = 0; k < 3; k++) {
-      m.sa[k] = s[1 + k];
-      m.sb[k] = s[4 + k];
+      for (int k = 0; k < 16; k++) rows[t][k] = s[k];
+      rows[t][16] = cnt;
     }
-#pragma unroll
-    for (int k = 0; k < 9; k++) m.sab[k] = s[7 + k];
   }
-  __shared__ CovSums sm[4];
-  const CovSums r = block_tree<CovSums, covsum_merge, covsum_identity>(m, sm);
+  __syncthreads();
+  const CovSums r = fold_rows(rows, gsum);
   CovSums* part = reinterpret_cast<CovSums*>(a.part);
   if (!FUSE) {
     if (t == 0) part[blockIdx.x] = r;
@@ -678,7 +732,7 @@ __global__ void __launch_bounds__(256) k_cull_waves(CullLaunch a, CovTail tail) 
   }
   __shared__ int last_s;
   if (!publish_part_last(part, r, tail.ticket, &last_s)) return;
-  const CovSums rr = block_tree_last_sc1<CovSums, covsum_merge, covsum_identity>(part, gridDim.x, sm);
+  const CovSums rr = fold_parts<true>(part, gridDim.x, rows, gsum);
   cov_last<false>(rr, a.it, const_cast<IterDev*>(a.it), tail);
 }
 
@@ -740,7 +794,7 @@ int64_t cull_num_blocks(int64_t n) { return ((n + 63) / 64 + kCullWaves - 1) / k
 hipError_t launch_cull_tail(const CullLaunch& a, unsigned* ticket, const IterPublish* pub, hipStream_t s) {
   const int64_t nb = cull_num_blocks(a.n);
   CovTail tail{nullptr, pub ? *pub : IterPublish{nullptr, nullptr, 0.0, nullptr, nullptr}, pub ? 1 : 0};
-  if (ticket && nb >= 1 && nb <= kFuseMaxBlocks && !a.loop) {  // one launch: the last block merges and publishes
+  if (ticket && nb >= 1 && nb <= kFuseMaxCullBlocks && !a.loop) {  // one launch: the last block merges and publishes
     tail.ticket = ticket;
     hipLaunchKernelGGL(k_cull_waves<true>, dim3((unsigned)nb), dim3(256), 0, s, a, tail);
     return hipGetLastError();

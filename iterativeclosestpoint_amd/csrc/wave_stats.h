@@ -22,57 +22,79 @@
 namespace icp {
 namespace dev {
 
-// doubles per lane row of the transposed reduction (9, not 8: the 8 lane groups' rows then fall
-// on two bank windows instead of one)
-constexpr int kStatStride = 9;
-constexpr int kStatLds = 64 * kStatStride * 8;  // bytes of LDS per wave (4.5 KB)
+constexpr int kStatLds = 64 * 4 * 8;  // bytes of LDS per wave (2 KB)
 
-// v ^ lane X within 32-lane groups (ds_swizzle bitmask mode: and 0x1f, xor X): LDS crossbar, no
-// vector ALU issue
-template <int X>
-__device__ __forceinline__ double swz_xor_d(double v) {
-  constexpr int kPat = 0x1f | (X << 10);
-  const long long b = __double_as_longlong(v);
-  const int lo = __builtin_amdgcn_ds_swizzle((int)(unsigned)b, kPat);
-  const int hi = __builtin_amdgcn_ds_swizzle((int)(b >> 32), kPat);
-  return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+// gfx950 v_permlane32_swap / v_permlane16_swap on a double: (x, y) -> (x', y') with
+//   32: x' = [x lanes 0-31, y lanes 0-31], y' = [x lanes 32-63, y lanes 32-63]
+//   16: x' = rows [x0, y0, x2, y2], y' = rows [x1, y1, x3, y3] (rows of 16 lanes)
+// Vector ALU instructions, one per dword: no LDS traffic.
+template <bool W32>
+__device__ __forceinline__ void swap_d(double& x, double& y) {
+  const long long bx = __double_as_longlong(x), by = __double_as_longlong(y);
+  const unsigned xl = (unsigned)bx, xh = (unsigned)(bx >> 32), yl = (unsigned)by, yh = (unsigned)(by >> 32);
+  unsigned nxl, nyl, nxh, nyh;
+  if (W32) {
+    const auto lo = __builtin_amdgcn_permlane32_swap(xl, yl, false, false);
+    const auto hi = __builtin_amdgcn_permlane32_swap(xh, yh, false, false);
+    nxl = lo[0], nyl = lo[1], nxh = hi[0], nyh = hi[1];
+  } else {
+    const auto lo = __builtin_amdgcn_permlane16_swap(xl, yl, false, false);
+    const auto hi = __builtin_amdgcn_permlane16_swap(xh, yh, false, false);
+    nxl = lo[0], nyl = lo[1], nxh = hi[0], nyh = hi[1];
+  }
+  x = __longlong_as_double((long long)(((unsigned long long)nxh << 32) | nxl));
+  y = __longlong_as_double((long long)(((unsigned long long)nyh << 32) | nyl));
 }
 
-// Sum over the wave of 8 values per lane, in a fixed order: every lane writes its row, lane
-// 8 k + p adds value k of rows 8 p .. 8 p + 7 in row order, then the 8 partial sums of value k
-// (lanes 8 k .. 8 k + 7) are added pairwise (p ^ 1, p ^ 2, p ^ 4; fp addition commutes, so every
-// lane of the group ends with the same bits). Returns value (lane >> 3)'s sum.
-__device__ __forceinline__ double wave_sum8(const double (&v)[8], double* lds, int lane) {
-  double* row = lds + lane * kStatStride;
+// Sum over the wave of 16 values per lane, in a fixed order; returns value (lane & 15)'s sum (the
+// four lanes holding a value hold the same bits). Reduce-scatter: value k and k + 8 swap halves
+// (lanes l, l + 32 added), then k and k + 4 swap rows (l, l + 16 added): row r of lanes then holds
+// values 4r .. 4r + 3, each summed over 4 lanes; the 16 partial sums of a value go through LDS
+// (2 KB per wave; lane l adds partials 4 (l >> 4) .. +3 of value l & 15 in order), and the four
+// quarters are added by a half swap and a row swap (commutative adds: equal bits everywhere).
+__device__ __forceinline__ double wave_sum16(double (&c)[16], double* lds, int lane) {
 #pragma unroll
-  for (int k = 0; k < 8; k++) row[k] = v[k];
+  for (int k = 0; k < 8; k++) {
+    swap_d<true>(c[k], c[k + 8]);
+    c[k] = c[k] + c[k + 8];
+  }
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    swap_d<false>(c[k], c[k + 4]);
+    c[k] = c[k] + c[k + 4];
+  }
+  // value-major blocks of 64, lane l's entry of register j at l ^ (4 j + (l >> 4)): the writes of
+  // a register are one contiguous 512 B, and the 64 reads of one step fall on 16 different 8-B
+  // bank pairs (4 lanes each, the minimum for 512 B) instead of 4
+#pragma unroll
+  for (int j = 0; j < 4; j++) lds[64 * j + (lane ^ (4 * j + (lane >> 4)))] = c[j];
   wave_lds_fence();
-  const double* col = lds + (8 * (lane & 7)) * kStatStride + (lane >> 3);
-  double acc = col[0];
+  const int v = lane & 15, q = lane >> 4, vr = v >> 2, vj = v & 3, key = 4 * vj + vr;
+  const double* blk = lds + 64 * vj;
+  const int s0 = 16 * vr + 4 * q;
+  double g = blk[s0 ^ key];
 #pragma unroll
-  for (int j = 1; j < 8; j++) acc += col[j * kStatStride];
-  acc += swz_xor_d<1>(acc);
-  acc += swz_xor_d<2>(acc);
-  acc += swz_xor_d<4>(acc);
-  wave_lds_fence();  // every read of the rows is done before they are rewritten
-  return acc;
+  for (int i = 1; i < 4; i++) g += blk[(s0 + i) ^ key];
+  wave_lds_fence();  // every read is done before the area is rewritten
+  double h = g;
+  swap_d<true>(g, h);
+  g = g + h;
+  h = g;
+  swap_d<false>(g, h);
+  return g + h;
 }
 
 // The canonical sums of the lanes with `in` (every lane of the wave calls it): 16 values,
 //   0 sum d^2, 1..3 sum (a - s), 4..6 sum (b - t), 7..15 sum (a - s)_r (b - t)_c (r-major)
 // (a = query, b = its match, (s, t) = the iterate's shift sh[0..5]; icpengine.cpp:76-90's H).
-// Lane 8 k + p returns value k in r1 and value 8 + k in r2. Lanes without `in` add +0.0.
-__device__ __forceinline__ void wave_cov_sums(bool in, double d, double qx, double qy, double qz, double mx,
-                                              double my, double mz, const double* sh, double* lds, int lane,
-                                              double& r1, double& r2) {
+// Returns value (lane & 15). Lanes without `in` add +0.0.
+__device__ __forceinline__ double wave_cov_sums(bool in, double d, double qx, double qy, double qz, double mx,
+                                                double my, double mz, const double* sh, double* lds, int lane) {
   const double da0 = in ? qx - sh[0] : 0.0, da1 = in ? qy - sh[1] : 0.0, da2 = in ? qz - sh[2] : 0.0;
   const double db0 = in ? mx - sh[3] : 0.0, db1 = in ? my - sh[4] : 0.0, db2 = in ? mz - sh[5] : 0.0;
-  {
-    const double v[8] = {in ? d * d : 0.0, da0, da1, da2, db0, db1, db2, da0 * db0};
-    r1 = wave_sum8(v, lds, lane);
-  }
-  const double v[8] = {da0 * db1, da0 * db2, da1 * db0, da1 * db1, da1 * db2, da2 * db0, da2 * db1, da2 * db2};
-  r2 = wave_sum8(v, lds, lane);
+  double c[16] = {in ? d * d : 0.0, da0, da1, da2, db0, db1, db2, da0 * db0,
+                  da0 * db1, da0 * db2, da1 * db0, da1 * db1, da1 * db2, da2 * db0, da2 * db1, da2 * db2};
+  return wave_sum16(c, lds, lane);
 }
 
 // One pair's terms added to a record's sums, in a fixed order (the cull kernel's band pairs).
