@@ -59,7 +59,7 @@ METRIC = "M correspondences/sec per ICP iter at 1/2/4/8 GPUs; final RMSE vs CPU 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
 # BASELINE.json configs by cloud size (config 3 is the LAS pair: tests/test_gpu_lasflow.py)
 CONFIG_NAMES = {100_000: "config2", 1_000_000: "synthetic-1M (config 3's size; config 3 itself, the LAS flow, is tests/test_gpu_lasflow.py)", 10_000_000: "config4", 50_000_000: "config5"}
-SEARCH_SOURCES = ("nn_kernels.hip", "nn_device.h", "kernels.h")
+SEARCH_SOURCES = ("nn_kernels.hip", "nn_device.h", "kernels.h", "wave_stats.h")
 # compulsory bytes of one k_nn_wave<true> launch
 STREAM_B_PER_QUERY = 24 + 24 + 4 + 4 + 8  # source read + transformed write, previous match (guess), pos + dist
 TGT_B_PER_POINT = 28  # x, y, z + original index of a leaf-ordered target point

@@ -22,7 +22,7 @@ with icp.Context(0, icp.config(debug_counters=1, timing_stride=1)) as ctx:
         sess.step()
     st = ctx.iterate(None, 1, icp.RULES_ENGINE, 3.0)
     import ctypes as C
-    out = np.zeros(24, np.uint64)
+    out = np.zeros(icp._lib.DBG_SLOTS, np.uint64)
     icp._lib._check(icp.lib().icp_hip_debug_counters(ctx.handle, icp._lib._ptr(out)))
     nn_ms, _ = ctx.last_timing()
     w = max(1, int(out[0]))
