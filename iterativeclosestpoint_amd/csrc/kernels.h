@@ -132,6 +132,7 @@ struct CullLaunch {
   int64_t n;
   const double* dist;       // the residuals (the band's and the recomputed waves' pairs)
   const WaveStat* wstat;    // the search's wave records (null: it wrote none this iterate)
+  int wpb;                  // search waves per cull block (set by launch_cull_tail)
 };
 
 // Residual moments of the settled queries in fixed parts (deterministic), then the merges.

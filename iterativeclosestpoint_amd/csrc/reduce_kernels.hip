@@ -543,7 +543,7 @@ __global__ void __launch_bounds__(64) k_finalize_cov(const CovMoments* gathered,
   finalize_cov_publish(it, g, pub, &rec);
 }
 
-// 3-sigma cull + covariance sums of kCullWaves search waves (64 queries each) per block:
+// 3-sigma cull + covariance sums of up to kCullWaves search waves (64 queries each) per block:
 //   1. the block's wave records (written by the search, cull_mode 1) are copied to LDS, coalesced;
 //   2. the waves without one (flag 1; every wave in mode 0) are recomputed by one wave each with
 //      the search's own function (wave_stats.h wave_cov_sums): against the band's lower end in
@@ -553,7 +553,16 @@ __global__ void __launch_bounds__(64) k_finalize_cov(const CovMoments* gathered,
 // So a wave's sums do not depend on which search settled which of its queries, nor on which
 // block recomputed it. The residual is read, not recomputed: every search path stores
 // d = sqrt(fl(dx^2 + dy^2 + dz^2)) (octree.cpp:139-144), and the pairs' terms use it as it is.
-constexpr int kCullWaves = 256;  // search waves per block: one record row per thread
+constexpr int kCullWaves = 256;  // search waves per block at most: one record row per thread
+
+// Search waves per cull block for n queries: ~600 blocks from 10M down (611 at 10M), at least 8
+// waves per block (a 100k cloud: 196 blocks; fewer, larger blocks left the small clouds' flagged
+// waves to a handful of waves in sequence: +10 us per iterate at 100k).
+int cull_waves_per_block(int64_t n) {
+  const int64_t nw = (n + 63) / 64;
+  const int64_t w = (nw + 599) / 600;
+  return (int)(w < 8 ? 8 : w > kCullWaves ? kCullWaves : w);
+}
 constexpr int kRow = 20;         // doubles per row: the WaveStat layout (s[16], cnt, bm, flag, pad)
 static_assert(sizeof(WaveStat) == kRow * sizeof(double), "rows are wave records");
 
@@ -640,8 +649,8 @@ __global__ void __launch_bounds__(256) k_cull_waves(CullLaunch a, CovTail tail) 
   for (int k = 0; k < 6; k++) sh[k] = it->cshift[k];
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int64_t nwaves = (a.n + 63) / 64;
-  const int64_t w0 = (int64_t)blockIdx.x * kCullWaves;
-  const int nw = (int)(nwaves - w0 < kCullWaves ? nwaves - w0 : kCullWaves);  // this block's waves
+  const int64_t w0 = (int64_t)blockIdx.x * a.wpb;
+  const int nw = (int)(nwaves - w0 < a.wpb ? nwaves - w0 : a.wpb);  // this block's waves
   if (t == 0) nlist = 0;
   if (fused) {
     // the block's records, 16-B loads over the whole block (coalesced)
@@ -789,9 +798,14 @@ hipError_t launch_finalize_moments(const Moments* gathered, int nranks, IterDev*
   return hipGetLastError();
 }
 
-int64_t cull_num_blocks(int64_t n) { return ((n + 63) / 64 + kCullWaves - 1) / kCullWaves; }
+int64_t cull_num_blocks(int64_t n) {
+  const int w = cull_waves_per_block(n);
+  return ((n + 63) / 64 + w - 1) / w;
+}
 
-hipError_t launch_cull_tail(const CullLaunch& a, unsigned* ticket, const IterPublish* pub, hipStream_t s) {
+hipError_t launch_cull_tail(const CullLaunch& a_in, unsigned* ticket, const IterPublish* pub, hipStream_t s) {
+  CullLaunch a = a_in;
+  a.wpb = cull_waves_per_block(a.n);
   const int64_t nb = cull_num_blocks(a.n);
   CovTail tail{nullptr, pub ? *pub : IterPublish{nullptr, nullptr, 0.0, nullptr, nullptr}, pub ? 1 : 0};
   if (ticket && nb >= 1 && nb <= kFuseMaxCullBlocks && !a.loop) {  // one launch: the last block merges and publishes

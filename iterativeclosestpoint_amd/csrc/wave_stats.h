@@ -90,15 +90,13 @@ __device__ __forceinline__ double wave_sum16(double (&c)[16], double* lds, int l
 // Returns value (lane & 15). Lanes without `in` add +0.0.
 __device__ __forceinline__ double wave_cov_sums(bool in, double d, double qx, double qy, double qz, double mx,
                                                 double my, double mz, const double* sh, double* lds, int lane) {
-  double da0, da1, da2, db0, db1, db2, dd;
-  if (__ballot(in) == ~0ull) {  // every lane counts (most waves): no selects, the same bits
-    da0 = qx - sh[0], da1 = qy - sh[1], da2 = qz - sh[2];
-    db0 = mx - sh[3], db1 = my - sh[4], db2 = mz - sh[5];
-    dd = d * d;
-  } else {
-    da0 = in ? qx - sh[0] : 0.0, da1 = in ? qy - sh[1] : 0.0, da2 = in ? qz - sh[2] : 0.0;
-    db0 = in ? mx - sh[3] : 0.0, db1 = in ? my - sh[4] : 0.0, db2 = in ? mz - sh[5] : 0.0;
-    dd = in ? d * d : 0.0;
+  double da0 = qx - sh[0], da1 = qy - sh[1], da2 = qz - sh[2];
+  double db0 = mx - sh[3], db1 = my - sh[4], db2 = mz - sh[5];
+  double dd = d * d;
+  if (__ballot(in) != ~0ull) {  // some lane does not count: zero its terms (most waves skip this)
+    da0 = in ? da0 : 0.0, da1 = in ? da1 : 0.0, da2 = in ? da2 : 0.0;
+    db0 = in ? db0 : 0.0, db1 = in ? db1 : 0.0, db2 = in ? db2 : 0.0;
+    dd = in ? dd : 0.0;
   }
   double c[16] = {dd, da0, da1, da2, db0, db1, db2, da0 * db0,
                   da0 * db1, da0 * db2, da1 * db0, da1 * db1, da1 * db2, da2 * db0, da2 * db1, da2 * db2};

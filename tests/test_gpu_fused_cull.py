@@ -55,8 +55,9 @@ def test_fused_cull_every_iterate_vs_oracle(icp, n, yaw):
 
 
 def test_fused_cull_equals_full_pass(icp):
-    """fused_cull 1 and 0 on the same trajectory: identical correspondences and valid counts,
-    statistics equal to the summation order."""
+    """fused_cull 1 and 0 on the same trajectory: the same correspondences and valid counts,
+    statistics equal to the summation order (so the transforms, and with them the moved queries'
+    residuals, may differ in their last bits from the second iterate on)."""
     tgt, src, _ = icp.synth_pair(500_000, yaw_deg=2.0)
     runs = []
     for fused in (1, 0):
@@ -72,7 +73,7 @@ def test_fused_cull_equals_full_pass(icp):
         runs.append(out)
     for k, ((ca, sa, pa), (cb, sb, pb)) in enumerate(zip(*runs)):
         np.testing.assert_array_equal(ca[0], cb[0])
-        np.testing.assert_array_equal(ca[1], cb[1])
+        np.testing.assert_allclose(ca[1], cb[1], rtol=1e-9, atol=1e-15)
         assert sa["valid"] == sb["valid"] and sa["n"] == sb["n"]
         for key in ("mean", "std", "threshold", "rmse"):
             np.testing.assert_allclose(sa[key], sb[key], rtol=1e-12)
@@ -155,3 +156,27 @@ def test_fused_cull_nonfinite_and_ragged(icp):
             np.testing.assert_allclose(sa["H"], sb["H"], rtol=1e-10, atol=1e-10 * max(1e-300, np.abs(sb["H"]).max()))
             if bad:
                 assert pa == 0  # NaN threshold: never a band
+
+
+@pytest.mark.parametrize("n", [100_000, 1_000_000])
+def test_fused_cull_is_deterministic(icp, n):
+    """Two contexts, the same inputs and history: bit-identical statistics every iterate (the
+    wave records, the recomputed waves, the band pairs and the folds are fixed-order)."""
+    tgt, src, _ = icp.synth_pair(n, yaw_deg=2.0)
+
+    def run():
+        out = []
+        with icp.Context(0) as ctx:
+            ctx.set_target(tgt, 10, 20, icp.RULES_ENGINE)
+            ctx.set_source(src)
+            T = None
+            for it in range(6):
+                st = ctx.iterate(T, it, icp.RULES_ENGINE, 3.0)
+                out.append(st.as_dict())
+                T = icp.best_fit_from_stats(st)
+        return out
+
+    a, b = run(), run()
+    for sa, sb in zip(a, b):
+        for key in sa:
+            np.testing.assert_array_equal(np.asarray(sa[key]), np.asarray(sb[key]), err_msg=key)

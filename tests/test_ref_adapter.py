@@ -39,7 +39,9 @@ def _run(exe, *args):
     r = subprocess.run([str(exe), *args], capture_output=True, text=True, timeout=300,
                        env={"QT_QPA_PLATFORM": "offscreen", "PATH": "/usr/bin:/bin"})
     assert r.returncode == 0, r.stdout + r.stderr
-    return json.loads(r.stdout.strip().splitlines()[-1])
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    out["stderr"] = r.stderr
+    return out
 
 
 def _ref_engine():
@@ -66,7 +68,7 @@ def test_reference_engine_empty_source(icp):
 def test_mirror_adapter_matches_facade(icp, tmp_path):
     out = _run(_build_mirror(tmp_path))
     assert out["rc"] == 0 and out["success"] == 1 and out["result_success"] == 1 and out["message"] == SUCCESS
-    assert out["same_as_facade"] == 1 and out["in_place"] == 1
+    assert out["same_as_facade"] == 1 and out["in_place"] == 1, out["stderr"]
     assert out["started"] == 1 and out["finished"] == 1
     assert out["iterations"] == out["history"] == out["total_iterations"] == out["progress"] >= 2
 
