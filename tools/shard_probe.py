@@ -18,7 +18,8 @@ from bench import shard_range
 n = int(os.environ.get("N", "10000000"))
 worlds = [int(w) for w in (sys.argv[1] if len(sys.argv) > 1 else "1,2,4,8").split(",")]
 tgt, src, _ = icp.synth_pair(n)
-ctx = icp.Context(0, icp.config(device_loop=int(os.environ.get("DEVICE_LOOP", "0")), timing_stride=1))
+device_loop = int(os.environ.get("DEVICE_LOOP", "0"))
+ctx = icp.Context(0, icp.config(device_loop=device_loop, timing_stride=1))
 ctx.set_target(tgt, 10, 20, icp.RULES_ENGINE)
 if os.environ.get("RCCL", "0") == "1":
     ctx.comm_init(1, 0, icp.Context.unique_id())
@@ -37,7 +38,7 @@ for w in worlds:
     ctx.synchronize()
     dt = (time.perf_counter() - t0) / k
     nn, it = ctx.timings(min(k, 256))
-    print(json.dumps({"world": w, "device_loop": int(os.environ.get("DEVICE_LOOP", "1")), "rccl": os.environ.get("RCCL", "0") == "1", "shard": hi - lo, "ms_per_step": round(dt * 1e3, 4),
+    print(json.dumps({"world": w, "device_loop": device_loop, "rccl": os.environ.get("RCCL", "0") == "1", "shard": hi - lo, "ms_per_step": round(dt * 1e3, 4),
                       "knn_ms": round(float(np.mean(nn)), 4), "iter_device_ms": round(float(np.mean(it)), 4),
                       "est_mcorr_s": round(n / dt / 1e6, 1)}), flush=True)
     sess.finish()
