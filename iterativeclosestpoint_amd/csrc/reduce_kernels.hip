@@ -548,7 +548,7 @@ __global__ void __launch_bounds__(64) k_finalize_cov(const CovMoments* gathered,
 //   2. the waves without one (flag 1; every wave in mode 0) are recomputed by one wave each with
 //      the search's own function (wave_stats.h wave_cov_sums): against the band's lower end in
 //      mode 1, against the threshold itself in mode 0 (no records, or the threshold left the band);
-//   3. each wave's band pairs (mode 1) with d <= thr are added in lane order;
+//   3. each wave's band pairs (mode 1) with d <= thr: one more canonical tree, added to its row;
 //   4. the block's column fold over its waves (fold_rows).
 // So a wave's sums do not depend on which search settled which of its queries, nor on which
 // block recomputed it. The residual is read, not recomputed: every search path stores
@@ -639,7 +639,8 @@ __global__ void __launch_bounds__(256) k_cull_waves(CullLaunch a, CovTail tail) 
   __shared__ __attribute__((aligned(32))) double red[4][kStatLds / 8];
   __shared__ double gsum[8 * 17];
   __shared__ int list[kCullWaves];
-  __shared__ int nlist;
+  __shared__ int blist[kCullWaves];
+  __shared__ int nlist, nblist;
   const IterDev* it = a.it;
   const double thr = it->thr;
   const bool fused = it->cull_mode != 0.0;
@@ -709,28 +710,37 @@ __global__ void __launch_bounds__(256) k_cull_waves(CullLaunch a, CovTail tail) 
     }
   }
   __syncthreads();
-  if (t < nw) {
-    unsigned long long bm = reinterpret_cast<const unsigned long long*>(rows[t])[17];
-    if (fused && bm) {
-      double s[16];
-#pragma unroll
-      for (int k = 0; k < 16; k++) s[k] = rows[t][k];
-      double cnt = rows[t][16];
-      const int64_t base = (w0 + t) * 64;
-      while (bm) {  // the band pairs below the threshold, in lane order
-        const int l = __builtin_ctzll(bm);
-        bm &= bm - 1ull;
-        const int64_t i = base + l;
-        const double d = a.dist[i];
-        if (d <= thr) {  // icpengine.cpp:265
-          const TgtPt* p = a.pts + a.pos[i];
-          add_pair(s, cnt, d, a.x[i], a.y[i], a.z[i], p->x, p->y, p->z, sh);
-        }
-      }
-#pragma unroll
-      for (int k = 0; k < 16; k++) rows[t][k] = s[k];
-      rows[t][16] = cnt;
+  // the band pairs below the threshold: per wave with band lanes, one more canonical tree (the
+  // same function, over its band lanes with d <= thr) added to its row, by one wave of the block
+  // each (the waves' band lanes in parallel, whatever their number)
+  if (t == 0) nblist = 0;
+  __syncthreads();
+  if (fused && t < nw && reinterpret_cast<const unsigned long long*>(rows[t])[17] != 0ull)
+    blist[atomicAdd(&nblist, 1)] = t;
+  __syncthreads();
+  const int nb = nblist;
+  for (int e = wv; e < nb; e += 4) {
+    const int tt = blist[e];
+    const unsigned long long bm = reinterpret_cast<const unsigned long long*>(rows[tt])[17];
+    const int64_t i = (w0 + tt) * 64 + lane;
+    const bool inb = (bm >> lane) & 1ull;  // band lanes are active lanes
+    const double d = inb ? a.dist[i] : 0.0;
+    const bool in = inb && d <= thr;  // icpengine.cpp:265
+    double qx = 0.0, qy = 0.0, qz = 0.0, mx = 0.0, my = 0.0, mz = 0.0;
+    if (in) {
+      qx = a.x[i];
+      qy = a.y[i];
+      qz = a.z[i];
+      const TgtPt* p = a.pts + a.pos[i];
+      const double2 xy = *reinterpret_cast<const double2*>(&p->x);
+      mx = xy.x;
+      my = xy.y;
+      mz = p->z;
     }
+    const double r = wave_cov_sums(in, d, qx, qy, qz, mx, my, mz, sh, red[wv], lane);
+    const int cnt = __popcll(__ballot(in));
+    if (lane < 16) rows[tt][lane] = rows[tt][lane] + r;
+    if (lane == 0) rows[tt][16] = rows[tt][16] + (double)cnt;
   }
   __syncthreads();
   const CovSums r = fold_rows(rows, gsum);

@@ -103,23 +103,5 @@ __device__ __forceinline__ double wave_cov_sums(bool in, double d, double qx, do
   return wave_sum16(c, lds, lane);
 }
 
-// One pair's terms added to a record's sums, in a fixed order (the cull kernel's band pairs).
-__device__ __forceinline__ void add_pair(double* s, double& cnt, double d, double qx, double qy, double qz, double mx,
-                                         double my, double mz, const double* sh) {
-  const double da[3] = {qx - sh[0], qy - sh[1], qz - sh[2]};
-  const double db[3] = {mx - sh[3], my - sh[4], mz - sh[5]};
-  cnt += 1.0;
-  s[0] += d * d;
-#pragma unroll
-  for (int r = 0; r < 3; r++) {
-    s[1 + r] += da[r];
-    s[4 + r] += db[r];
-  }
-#pragma unroll
-  for (int r = 0; r < 3; r++)
-#pragma unroll
-    for (int c = 0; c < 3; c++) s[7 + 3 * r + c] += da[r] * db[c];
-}
-
 }  // namespace dev
 }  // namespace icp
