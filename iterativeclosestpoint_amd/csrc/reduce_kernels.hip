@@ -570,16 +570,18 @@ static_assert(sizeof(WaveStat) == kRow * sizeof(double), "rows are wave records"
 // index in a row.
 __device__ __forceinline__ int row_col(int v) { return v == 0 ? 16 : v - 1; }
 
-// The fixed-order column sums of 256 rows (LDS): thread 17 g + v (g < 8) adds column v of rows
-// 32 g .. 32 g + 31 in order, then thread v adds the 8 group sums in order. Every thread of the
-// (256-thread) block calls it; the result is the same for all.
-__device__ CovSums fold_rows(const double (*rows)[kRow], double* gsum) {
+// The fixed-order column sums of the first `nrows` (<= 256, block-uniform) rows (LDS): thread
+// 17 g + v (g < 8) adds column v of rows 32 g .. min(32 g + 31, nrows - 1) in order (0 for an
+// empty group), then thread v adds the 8 group sums in order. Every thread of the (256-thread)
+// block calls it; the result is the same for all. (A small cloud's cull blocks hold 8 waves:
+// their fold reads those 8 rows, not 256.)
+__device__ CovSums fold_rows(const double (*rows)[kRow], double* gsum, int nrows = 256) {
   const int t = threadIdx.x;
   if (t < 8 * 17) {
     const int g = t / 17, v = t % 17, c = row_col(v);
-    double acc = rows[32 * g][c];
-#pragma unroll 8
-    for (int i = 1; i < 32; i++) acc += rows[32 * g + i][c];
+    const int r0 = 32 * g, r1 = r0 + 32 < nrows ? r0 + 32 : nrows;
+    double acc = r0 < r1 ? rows[r0][c] : 0.0;
+    for (int i = r0 + 1; i < r1; i++) acc += rows[i][c];
     gsum[g * 17 + v] = acc;
   }
   __syncthreads();
@@ -743,7 +745,7 @@ __global__ void __launch_bounds__(256) k_cull_waves(CullLaunch a, CovTail tail) 
     if (lane == 0) rows[tt][16] = rows[tt][16] + (double)cnt;
   }
   __syncthreads();
-  const CovSums r = fold_rows(rows, gsum);
+  const CovSums r = fold_rows(rows, gsum, a.wpb);
   CovSums* part = reinterpret_cast<CovSums*>(a.part);
   if (!FUSE) {
     if (t == 0) part[blockIdx.x] = r;
