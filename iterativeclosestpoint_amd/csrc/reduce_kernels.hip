@@ -555,9 +555,10 @@ __global__ void __launch_bounds__(64) k_finalize_cov(const CovMoments* gathered,
 // d = sqrt(fl(dx^2 + dy^2 + dz^2)) (octree.cpp:139-144), and the pairs' terms use it as it is.
 constexpr int kCullWaves = 256;  // search waves per block at most: one record row per thread
 
-// Search waves per cull block for n queries: ~600 blocks from 10M down (611 at 10M), at least 8
-// waves per block (a 100k cloud: 196 blocks; fewer, larger blocks left the small clouds' flagged
-// waves to a handful of waves in sequence: +10 us per iterate at 100k).
+// Search waves per cull block for n queries: ~600 blocks up to 10M (611 at 10M; beyond, 256
+// waves per block: 3052 blocks at 50M), at least 8 waves per block (a 100k cloud: 196 blocks;
+// fewer, larger blocks left the small clouds' flagged waves to a handful of waves in sequence:
+// +10 us per iterate at 100k).
 int cull_waves_per_block(int64_t n) {
   const int64_t nw = (n + 63) / 64;
   const int64_t w = (nw + 599) / 600;
