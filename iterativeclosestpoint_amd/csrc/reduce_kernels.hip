@@ -548,12 +548,32 @@ __global__ void __launch_bounds__(64) k_finalize_cov(const CovMoments* gathered,
 //   2. the waves without one (flag 1; every wave in mode 0) are recomputed by one wave each with
 //      the search's own function (wave_stats.h wave_cov_sums): against the band's lower end in
 //      mode 1, against the threshold itself in mode 0 (no records, or the threshold left the band);
-//   3. each wave's band pairs (mode 1) with d <= thr: one more canonical tree, added to its row;
+//   3. each wave's band pairs (mode 1) with d <= thr: added in lane order by its thread, or (many
+//      band lanes) as one more canonical tree by a wave;
 //   4. the block's column fold over its waves (fold_rows).
 // So a wave's sums do not depend on which search settled which of its queries, nor on which
 // block recomputed it. The residual is read, not recomputed: every search path stores
 // d = sqrt(fl(dx^2 + dy^2 + dz^2)) (octree.cpp:139-144), and the pairs' terms use it as it is.
 constexpr int kCullWaves = 256;  // search waves per block at most: one record row per thread
+constexpr int kSeqBand = 8;      // band lanes a thread adds itself; more: a wave's tree
+
+// One pair's terms added to a record row (16 sums in the record's order, then the count).
+__device__ __forceinline__ void add_pair(double* row, double d, double qx, double qy, double qz, double mx, double my,
+                                         double mz, const double* sh) {
+  const double da[3] = {qx - sh[0], qy - sh[1], qz - sh[2]};
+  const double db[3] = {mx - sh[3], my - sh[4], mz - sh[5]};
+  row[0] += d * d;
+#pragma unroll
+  for (int r = 0; r < 3; r++) {
+    row[1 + r] += da[r];
+    row[4 + r] += db[r];
+  }
+#pragma unroll
+  for (int r = 0; r < 3; r++)
+#pragma unroll
+    for (int c = 0; c < 3; c++) row[7 + 3 * r + c] += da[r] * db[c];
+  row[16] += 1.0;
+}
 
 // Search waves per cull block for n queries: ~600 blocks up to 10M (611 at 10M; beyond, 256
 // waves per block: 3052 blocks at 50M), at least 8 waves per block (a 100k cloud: 196 blocks;
@@ -713,13 +733,32 @@ __global__ void __launch_bounds__(256) k_cull_waves(CullLaunch a, CovTail tail) 
     }
   }
   __syncthreads();
-  // the band pairs below the threshold: per wave with band lanes, one more canonical tree (the
-  // same function, over its band lanes with d <= thr) added to its row, by one wave of the block
-  // each (the waves' band lanes in parallel, whatever their number)
+  // the band pairs below the threshold. A wave with at most kSeqBand band lanes: its thread adds
+  // them to its row in lane order (one gather chain each, usually 0 or 1); a wave with more: one
+  // more canonical tree (the same function, over its band lanes with d <= thr) added to its row
+  // by one wave of the block (its band lanes in parallel). Which one is a function of the wave's
+  // band mask, so the bits stay a function of the data.
   if (t == 0) nblist = 0;
   __syncthreads();
-  if (fused && t < nw && reinterpret_cast<const unsigned long long*>(rows[t])[17] != 0ull)
-    blist[atomicAdd(&nblist, 1)] = t;
+  if (fused && t < nw) {
+    unsigned long long bm = reinterpret_cast<const unsigned long long*>(rows[t])[17];
+    if (__popcll(bm) > kSeqBand) {
+      blist[atomicAdd(&nblist, 1)] = t;
+    } else if (bm) {
+      double* row = rows[t];
+      const int64_t base = (w0 + t) * 64;
+      while (bm) {
+        const int l = __builtin_ctzll(bm);
+        bm &= bm - 1ull;
+        const int64_t i = base + l;
+        const double d = a.dist[i];
+        if (d <= thr) {  // icpengine.cpp:265
+          const TgtPt* p = a.pts + a.pos[i];
+          add_pair(row, d, a.x[i], a.y[i], a.z[i], p->x, p->y, p->z, sh);
+        }
+      }
+    }
+  }
   __syncthreads();
   const int nb = nblist;
   for (int e = wv; e < nb; e += 4) {
