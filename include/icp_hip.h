@@ -37,7 +37,8 @@ extern "C" {
 #define ICP_HIP_EDEVICE (-3)
 #define ICP_HIP_ERCCL (-4)
 #define ICP_HIP_ENOTREADY (-5)
-#define ICP_HIP_EEXCHANGE (-6) /* the host-exchange callback (icp_hip_comm_init_host) failed */
+#define ICP_HIP_EEXCHANGE (-6) /* the host-exchange callback (icp_hip_comm_init_host) failed or
+                                  overran config.peer_timeout_ms */
 
 #define ICP_HIP_UNIQUE_ID_BYTES 128
 
@@ -127,7 +128,21 @@ typedef struct icp_hip_config {
                               waves the search left to its other paths (icp_hip_last_cull_path);
                               0: every cull is a full pass. The same valid pairs either way; the
                               sums differ in their order only                             dflt 1 */
+  int32_t peer_timeout_ms; /* multi-rank iterates (comm_init / comm_init_host): the longest the host
+                              waits for an iterate whose record exchange involves peers. Past it
+                              the iterate fails (RCCL: ICP_HIP_ERCCL after ncclCommAbort, so the
+                              pending collective returns and the stream drains; host exchange:
+                              ICP_HIP_EEXCHANGE, the callback left running on the context's
+                              exchange thread) and every later iterate fails with ICP_HIP_ERCCL
+                              until comm_init / comm_init_host. 0: no deadline. Independently of
+                              it, an RCCL communicator's asynchronous error (a peer process that
+                              died, a broken link: ncclCommGetAsyncError) is checked while the
+                              host waits, with the same outcome                           dflt 0 */
+  int32_t reserved[6];     /* zero (fields of later versions of this header)                    */
+  uint32_t config_version; /* ICP_HIP_CONFIG_VERSION, set by icp_hip_config_default; create_ex
+                              rejects any other value (a struct from another header version)     */
 } icp_hip_config;
+#define ICP_HIP_CONFIG_VERSION 2u /* 1: r4 and earlier (no peer_timeout_ms, no version field) */
 
 /* Slots of icp_hip_debug_counters (summed over the last iterate's search launches). */
 #define ICP_DBG_WAVES 0          /* waves of the wave search                                  */
@@ -262,8 +277,15 @@ int icp_hip_comm_init_host(icp_hip_ctx* ctx, int nranks, int rank, icp_hip_excha
 /* Abort this rank's RCCL communicator (ncclCommAbort): collectives it has enqueued that a failed
  * peer will never join return, so the stream drains and icp_hip_destroy cannot block. For a
  * rank whose peer failed (one process per GPU; the multi-device context does this itself). The
- * context's iterate then fails with ICP_HIP_ERCCL until comm_init / comm_init_host is called
- * again. No communicator: nothing to do. */
+ * context's iterates (icp_hip_iterate and the device-resident loop of icp_session_step_n /
+ * icp_engine_run) then fail with ICP_HIP_ERCCL until comm_init / comm_init_host is called
+ * again. No communicator: nothing to do.
+ * Peer failure without a call to this function: while the host waits for a multi-rank iterate
+ * it checks the communicator's asynchronous error and config.peer_timeout_ms, and on either
+ * aborts the communicator itself (the iterate returns ICP_HIP_ERCCL). A host-exchange callback
+ * that overruns config.peer_timeout_ms makes the iterate return ICP_HIP_EEXCHANGE; the callback
+ * keeps running on the context's exchange thread and must return eventually: comm_init,
+ * comm_init_host and icp_hip_destroy wait for it. */
 int icp_hip_comm_abort(icp_hip_ctx* ctx);
 
 /* Build the reference octree of the target (AoS xyz, n points) and keep it in HBM. The tree is

@@ -15,6 +15,7 @@
 #include <cstdlib>
 #include <cstdio>
 #include <atomic>
+#include <chrono>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -158,6 +159,8 @@ void icp_hip_config_default(icp_hip_config* cfg) {
   cfg->overflow_halves = 1;
   cfg->device_loop = 0;
   cfg->timing_stride = 0;
+  cfg->peer_timeout_ms = 0;
+  cfg->config_version = ICP_HIP_CONFIG_VERSION;
 }
 
 int icp_hip_create(icp_hip_ctx** out, int device) { return icp_hip_create_ex(out, device, nullptr); }
@@ -168,6 +171,10 @@ int icp_hip_create_ex(icp_hip_ctx** out, int device, const icp_hip_config* cfg) 
   icp_hip_config conf;
   icp_hip_config_default(&conf);
   if (cfg) conf = *cfg;
+  if (conf.config_version != ICP_HIP_CONFIG_VERSION)
+    return fail(ICP_HIP_EINVAL, "config: config_version is not ICP_HIP_CONFIG_VERSION (start from icp_hip_config_default "
+                                "of this header)");
+  if (conf.peer_timeout_ms < 0) return fail(ICP_HIP_EINVAL, "config: peer_timeout_ms must be >= 0");
   if (conf.search != ICP_SEARCH_CERTIFIED && conf.search != ICP_SEARCH_REFERENCE)
     return fail(ICP_HIP_EINVAL, "config: unknown search");
   if (conf.octree_builder != ICP_BUILD_AUTO && conf.octree_builder != ICP_BUILD_HOST)
@@ -257,7 +264,7 @@ void icp_hip_destroy(icp_hip_ctx* c) {
   if (c->h_loop) (void)hipHostFree(c->h_loop);
   if (c->h_ring) (void)hipHostFree(c->h_ring);
   if (c->ev_batch) (void)hipEventDestroy(c->ev_batch);
-  if (c->comm) (void)ncclCommDestroy(c->comm);
+  icp_ctx_drop_transport(c);
   for (hipEvent_t ev : {c->ev_it0, c->ev_it1})
     if (ev) (void)hipEventDestroy(ev);
   for (auto& r : c->ring)
@@ -280,13 +287,7 @@ int icp_hip_comm_init(icp_hip_ctx* c, int nranks, int rank, const uint8_t id_byt
   if (!c || !id_bytes || nranks < 1 || rank < 0 || rank >= nranks) return fail(ICP_HIP_EINVAL, "bad comm arguments");
   HIP_TRY(hipSetDevice(c->device));
   // back to a world of one first: a failure below leaves no stale transport behind
-  if (c->comm) (void)ncclCommDestroy(c->comm);
-  c->comm = nullptr;
-  c->comm_aborted = false;
-  c->xfn = nullptr;
-  c->xuser = nullptr;
-  c->nranks = 1;
-  c->rank = 0;
+  icp_ctx_drop_transport(c);
   dfree(c->gm);
   dfree(c->gc);
   HIP_TRY(dalloc(&c->gm, (size_t)nranks));
@@ -303,6 +304,18 @@ int icp_hip_comm_init(icp_hip_ctx* c, int nranks, int rank, const uint8_t id_byt
 
 }  // extern "C"
 
+void icp_ctx_drop_transport(icp_hip_ctx* c) {
+  if (c->comm) (void)ncclCommDestroy(c->comm);
+  c->comm = nullptr;
+  delete c->xworker;  // waits for a callback that overran the deadline to return
+  c->xworker = nullptr;
+  c->comm_aborted = false;
+  c->xfn = nullptr;
+  c->xuser = nullptr;
+  c->nranks = 1;
+  c->rank = 0;
+}
+
 void icp_ctx_abort_comm(icp_hip_ctx* c) {
   if (!c->comm) return;
   (void)hipSetDevice(c->device);
@@ -317,13 +330,7 @@ void icp_ctx_abort_comm(icp_hip_ctx* c) {
 
 int icp_ctx_attach_comm(icp_hip_ctx* c, ncclComm_t comm, int nranks, int rank) {
   HIP_TRY(hipSetDevice(c->device));
-  if (c->comm) (void)ncclCommDestroy(c->comm);
-  c->comm = nullptr;
-  c->comm_aborted = false;
-  c->xfn = nullptr;
-  c->xuser = nullptr;
-  c->nranks = 1;
-  c->rank = 0;
+  icp_ctx_drop_transport(c);
   dfree(c->gm);
   dfree(c->gc);
   HIP_TRY(dalloc(&c->gm, (size_t)nranks));
@@ -341,13 +348,7 @@ int icp_hip_comm_init_host(icp_hip_ctx* c, int nranks, int rank, icp_hip_exchang
   if (!c || nranks < 1 || rank < 0 || rank >= nranks || (nranks > 1 && !exchange))
     return fail(ICP_HIP_EINVAL, "bad comm arguments");
   HIP_TRY(hipSetDevice(c->device));
-  if (c->comm) (void)ncclCommDestroy(c->comm);
-  c->comm = nullptr;
-  c->comm_aborted = false;
-  c->xfn = nullptr;
-  c->xuser = nullptr;
-  c->nranks = 1;
-  c->rank = 0;
+  icp_ctx_drop_transport(c);
   if (!exchange) return ICP_HIP_OK;  // a world of one without a transport
   dfree(c->gm);
   dfree(c->gc);
@@ -370,8 +371,20 @@ static int all_gather_record(icp_hip_ctx* c, const double* d_local, double* d_ga
   std::vector<double> local((size_t)count), all((size_t)count * c->nranks);
   HIP_TRY(hipMemcpyAsync(local.data(), d_local, sizeof(double) * count, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
-  if (c->xfn(c->xuser, local.data(), count, all.data()) != 0)
+  if (c->cfg.peer_timeout_ms > 0) {
+    // the callback on the exchange thread, given up on at the deadline (it cannot be interrupted:
+    // it finishes on that thread, and comm_init / comm_init_host / destroy wait for it)
+    if (!c->xworker) c->xworker = new ExchangeWorker();
+    if (c->xworker->run(c->xfn, c->xuser, local.data(), count, c->nranks, c->cfg.peer_timeout_ms) != 0) {
+      c->comm_aborted = true;
+      return fail(ICP_HIP_EEXCHANGE, "host exchange callback overran config.peer_timeout_ms (" +
+                                         std::to_string(c->cfg.peer_timeout_ms) + " ms); comm_init_host again");
+    }
+    if (c->xworker->rc != 0) return fail(ICP_HIP_EEXCHANGE, "host exchange callback failed");
+    all.swap(c->xworker->all);
+  } else if (c->xfn(c->xuser, local.data(), count, all.data()) != 0) {
     return fail(ICP_HIP_EEXCHANGE, "host exchange callback failed");
+  }
   HIP_TRY(hipMemcpyAsync(d_gathered, all.data(), sizeof(double) * all.size(), hipMemcpyHostToDevice, s));
   HIP_TRY(hipStreamSynchronize(s));
   return ICP_HIP_OK;
@@ -583,6 +596,45 @@ int icp_hip_set_source(icp_hip_ctx* c, const double* xyz, int64_t n) {
 
 }  // extern "C"
 
+// The host's wait for the device (the only wait of an iterate or of a device-loop batch): `done`
+// polled in a tight loop; every 1024 polls the group's abort flag, the stream's own errors and,
+// with peers (an RCCL communicator or the host exchange), the communicator's asynchronous error
+// and config.peer_timeout_ms. A peer process that died or a broken link leaves this rank's
+// ncclAllGather waiting forever on the device: RCCL reports it as the communicator's async error,
+// and the deadline covers what it does not see. Either way the communicator is aborted (the
+// pending collective returns, the stream drains) and iterates fail with ERCCL until comm_init.
+template <class Done>
+static int wait_device(icp_hip_ctx* c, Done done, const char* what) {
+  hipStream_t s = c->stream;
+  const bool peers = c->comm != nullptr || (c->xfn != nullptr && c->nranks > 1);
+  const auto t0 = std::chrono::steady_clock::now();
+  for (unsigned spin = 1; !done(); spin++) {
+    if ((spin & 1023u) != 0) continue;
+    if (c->abort && c->abort->load()) return fail(ICP_HIP_EEXCHANGE, std::string(what) + ": a peer device of the group failed");
+    if (c->comm) {
+      ncclResult_t ae = ncclSuccess;
+      if (ncclCommGetAsyncError(c->comm, &ae) == ncclSuccess && ae != ncclSuccess && ae != ncclInProgress) {
+        icp_ctx_abort_comm(c);
+        return fail(ICP_HIP_ERCCL, std::string(what) + ": the communicator failed (" + ncclGetErrorString(ae) +
+                                       "; a peer rank died or a link broke): communicator aborted, comm_init again");
+      }
+    }
+    if (peers && c->cfg.peer_timeout_ms > 0 &&
+        std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(c->cfg.peer_timeout_ms)) {
+      if (c->comm) icp_ctx_abort_comm(c);
+      c->comm_aborted = true;
+      return fail(ICP_HIP_ERCCL, std::string(what) + ": no record within config.peer_timeout_ms (" +
+                                     std::to_string(c->cfg.peer_timeout_ms) +
+                                     " ms; a peer rank stalled or died): communicator aborted, comm_init again");
+    }
+    const hipError_t q = hipStreamQuery(s);
+    if (q == hipSuccess && done()) break;
+    if (q == hipSuccess) return fail(ICP_HIP_EDEVICE, std::string(what) + ": stream idle but the record was not published");
+    if (q != hipErrorNotReady) return fail(ICP_HIP_EDEVICE, std::string(what) + ": " + hipGetErrorString(q));
+  }
+  return ICP_HIP_OK;
+}
+
 // One iterate enqueued on the context's stream, no wait. Host-driven (loop_slot < 0): the
 // transform T_apply (null: none) is a kernel argument and the last kernel publishes the record
 // with sequence number *seq for the host's poll. Device loop (loop_slot >= 0): the transform is
@@ -590,6 +642,8 @@ int icp_hip_set_source(icp_hip_ctx* c, const double* xyz, int64_t n) {
 // and stores the iteration's LoopRec into ring slot loop_slot.
 static int enqueue_iterate(icp_hip_ctx* c, const double* T_apply, bool apply, int iter, int rules,
                            double sigma_multiplier, int loop_slot, uint64_t* seq_out) {
+  if (c->comm_aborted)
+    return fail(ICP_HIP_ERCCL, "iterate: the communicator was aborted (icp_hip_comm_abort or a peer failure); comm_init again");
   hipStream_t s = c->stream;
   hipEvent_t* ev = c->ring[c->n_iterates % icp_hip_ctx::kTimingRing];
   LoopDev* loop = loop_slot >= 0 ? c->loopd : nullptr;
@@ -693,9 +747,7 @@ int icp_hip_iterate(icp_hip_ctx* c, const double* T_apply, int iter, int rules, 
   if (c->group) return group_iterate(c, T_apply, iter, rules, sigma_multiplier, out);
   if (!c->nodes) return fail(ICP_HIP_ENOTREADY, "target not set");
   if (!c->x && c->n_src > 0) return fail(ICP_HIP_ENOTREADY, "source not set");
-  if (c->comm_aborted) return fail(ICP_HIP_ERCCL, "iterate: the communicator was aborted (icp_hip_comm_abort); comm_init again");
   HIP_TRY(hipSetDevice(c->device));
-  hipStream_t s = c->stream;
   uint64_t seq = 0;
   const int rc = enqueue_iterate(c, T_apply, T_apply != nullptr, iter, rules, sigma_multiplier, -1, &seq);
   if (rc != ICP_HIP_OK) return rc;
@@ -709,16 +761,8 @@ int icp_hip_iterate(icp_hip_ctx* c, const double* T_apply, int iter, int rules, 
     uint64_t want_bits;
     std::memcpy(&want_bits, &want, sizeof(want));
     const uint64_t* word = reinterpret_cast<const uint64_t*>(&c->h_it->pad[3]);
-    auto published = [&]() { return __atomic_load_n(word, __ATOMIC_ACQUIRE) == want_bits; };
-    for (unsigned spin = 1; !published(); spin++) {
-      if ((spin & 1023u) == 0) {
-        if (c->abort && c->abort->load()) return fail(ICP_HIP_EEXCHANGE, "iterate: a peer device of the group failed");
-        const hipError_t q = hipStreamQuery(s);
-        if (q == hipSuccess && published()) break;
-        if (q == hipSuccess) return fail(ICP_HIP_EDEVICE, "iterate: stream idle but the record was not published");
-        if (q != hipErrorNotReady) return fail(ICP_HIP_EDEVICE, std::string("iterate: ") + hipGetErrorString(q));
-      }
-    }
+    const int wrc = wait_device(c, [&]() { return __atomic_load_n(word, __ATOMIC_ACQUIRE) == want_bits; }, "iterate");
+    if (wrc != ICP_HIP_OK) return wrc;
   }
   c->lists_zero = true;
   for (int k = 0; k < 3; k++) c->last_lists[k] = (unsigned int)c->h_it->pad[k];
@@ -775,6 +819,10 @@ int icp_hip_loop_run(icp_hip_ctx* c, icp::SessionCore* core, const icp::SessionP
     if (rc != ICP_HIP_OK) return rc;
   }
   HIP_TRY(hipMemcpyAsync(c->h_loop, c->loopd, sizeof(LoopDev), hipMemcpyDeviceToHost, s));
+  // (polled rather than hipStreamSynchronize: a batch over a communicator whose peer died would
+  // otherwise wait forever)
+  const int wrc = wait_device(c, [&]() { return hipStreamQuery(s) != hipErrorNotReady; }, "device loop");
+  if (wrc != ICP_HIP_OK) return wrc;
   const hipError_t e = hipStreamSynchronize(s);
   if (e != hipSuccess) return fail(ICP_HIP_EDEVICE, std::string("device loop: ") + hipGetErrorString(e));
   *core = c->h_loop->core;

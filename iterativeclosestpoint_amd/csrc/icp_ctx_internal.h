@@ -5,10 +5,72 @@
 #include <rccl/rccl.h>
 
 #include <atomic>
+#include <chrono>
+#include <condition_variable>
 #include <cstdint>
+#include <mutex>
+#include <thread>
+#include <vector>
 
 #include "../../include/icp_hip.h"
 #include "kernels.h"
+
+// The host-exchange callback run on a thread of its own, so that the iterate can give up on it
+// at config.peer_timeout_ms (the callback is the caller's code: it cannot be interrupted, only
+// abandoned). One job at a time; an abandoned job finishes on its own, and join() (comm_init,
+// comm_init_host, destroy) waits for it.
+struct ExchangeWorker {
+  std::mutex m;
+  std::condition_variable cv;
+  std::thread th;
+  bool job = false, done = false, quit = false;
+  icp_hip_exchange_fn fn = nullptr;
+  void* user = nullptr;
+  std::vector<double> local, all;
+  int count = 0, rc = 0;
+
+  ExchangeWorker() {
+    th = std::thread([this] {
+      std::unique_lock<std::mutex> lk(m);
+      while (true) {
+        cv.wait(lk, [this] { return job || quit; });
+        if (quit && !job) return;
+        lk.unlock();
+        const int r = fn(user, local.data(), count, all.data());
+        lk.lock();
+        rc = r;
+        job = false;
+        done = true;
+        cv.notify_all();
+      }
+    });
+  }
+  // The callback on this rank's record; 0 = done in time (gathered in `all`), 1 = the deadline
+  // passed first (the job stays with the thread).
+  int run(icp_hip_exchange_fn f, void* u, const double* rec, int n, int nranks, int timeout_ms) {
+    std::unique_lock<std::mutex> lk(m);
+    cv.wait(lk, [this] { return !job; });  // an abandoned job first
+    fn = f;
+    user = u;
+    count = n;
+    local.assign(rec, rec + n);
+    all.assign((size_t)n * nranks, 0.0);
+    done = false;
+    job = true;
+    cv.notify_all();
+    if (!cv.wait_for(lk, std::chrono::milliseconds(timeout_ms), [this] { return done; })) return 1;
+    return 0;
+  }
+  void join() {
+    {
+      std::lock_guard<std::mutex> lk(m);
+      quit = true;
+    }
+    cv.notify_all();
+    if (th.joinable()) th.join();
+  }
+  ~ExchangeWorker() { join(); }
+};
 
 struct icp_hip_ctx {
   int device = 0;
@@ -81,6 +143,7 @@ struct icp_hip_ctx {
   ncclComm_t comm = nullptr;
   icp_hip_exchange_fn xfn = nullptr;  // host exchange instead of RCCL (icp_hip_comm_init_host)
   void* xuser = nullptr;
+  ExchangeWorker* xworker = nullptr;  // runs xfn when config.peer_timeout_ms > 0
   icp::Moments* gm = nullptr;
   icp::CovMoments* gc = nullptr;
   // a member of a multi-device context: set when a peer member failed (the waits give up)
@@ -109,6 +172,9 @@ int icp_hip_loop_run(icp_hip_ctx* c, icp::SessionCore* core, const icp::SessionP
 int icp_ctx_attach_comm(icp_hip_ctx* c, ncclComm_t comm, int nranks, int rank);
 // ncclCommAbort of the context's communicator (icp_hip_comm_abort without the argument checks)
 void icp_ctx_abort_comm(icp_hip_ctx* c);
+// Back to a world of one without a transport: the communicator destroyed, the exchange thread
+// joined (after its callback returns), comm_aborted cleared.
+void icp_ctx_drop_transport(icp_hip_ctx* c);
 
 // The multi-device context (icp_group.cpp): every C-ABI entry point of icp_ctx.hip dispatches here
 // when ctx->group is set.

@@ -624,7 +624,7 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
         const double ex = (((T[0] * cx + T[1] * cy) + T[2] * cz) + T[3]) - cx;
         const double ey = (((T[4] * cx + T[5] * cy) + T[6] * cz) + T[7]) - cy;
         const double ez = (((T[8] * cx + T[9] * cy) + T[10] * cz) + T[11]) - cz;
-        // finite and at most B's largest extent per iterate (a wild increment leads nowhere)
+        // finite and at most twice B's largest extent per iterate (a wild increment leads nowhere)
         const double cap = 2.0 * dmax_(dmax_(bhx - blx, bhy - bly), bhz - blz);
         auto lead = [&](double e) { return (e == e && __builtin_fabs(e) <= cap) ? a.wc_lead * e : 0.0; };
         const double lx = lead(ex), ly = lead(ey), lz = lead(ez);

@@ -1,5 +1,7 @@
 """Multi-rank path on CPU (world_size 2, gloo): the exchange step of the sharded registration.
 
+Shards are what the product uses: contiguous ranges of the source's kd order
+(icp_source_shard_order, include/icp_host.h; bench.py and icp_group.cpp), spatially compact.
 On the GPU each rank reduces its shard to one Moments and one CovMoments record, all-gathers
 them over RCCL and merges them in rank order on the device. Here the same records are built by
 the product's host functions from each rank's shard (residuals from the CPU oracle, the test
@@ -49,8 +51,10 @@ def _worker(rank, world, port, n, q):
 
     dist.init_process_group("gloo", rank=rank, world_size=world)
     tgt, src, _ = icp.synth_pair(n, yaw_deg=3.0)
+    # the product's sharding (bench.py, icp_group.cpp): rank r takes a contiguous range of the
+    # kd order of the source (icp_source_shard_order), a spatially compact shard
     lo, hi = shard_range(n, rank, world)
-    shard = src[lo:hi]
+    shard = src[icp.source_shard_order(src)[lo:hi]]
     idx, d = oracle_py.OracleTree(tgt).nn(shard, init_best=oracle_py.DBL_MAX)
 
     def gather(vec):
@@ -98,6 +102,23 @@ def test_sharded_exchange_matches_single_process(icp, oracle, world):
         np.testing.assert_allclose(T, T_ref, atol=1e-12)
     # bitwise identical across ranks
     assert all(np.array_equal(results[0][4], r[4]) for r in results)
+
+
+def test_kd_shards_are_spatially_compact(icp):
+    """The kd-order shards partition the source, and each rank's shard is spatially compact:
+    the shards' bounding boxes are far smaller than the cloud's (contiguous ranges of the shuffled
+    cloud would each span all of it)."""
+    sys.path.insert(0, str(ROOT))
+    from bench import shard_range
+    n, world = 20000, 4
+    _, src, _ = icp.synth_pair(n, yaw_deg=3.0)
+    order = icp.source_shard_order(src)
+    assert np.array_equal(np.sort(order), np.arange(n))
+    vol = lambda a: float(np.prod(a.max(0) - a.min(0)))
+    for r in range(world):
+        lo, hi = shard_range(n, r, world)
+        assert vol(src[order[lo:hi]]) < 0.6 * vol(src)
+        assert vol(src[lo:hi]) > 0.8 * vol(src)
 
 
 def test_shard_range_partitions():

@@ -180,3 +180,65 @@ def test_fused_cull_is_deterministic(icp, n):
     for sa, sb in zip(a, b):
         for key in sa:
             np.testing.assert_array_equal(np.asarray(sa[key]), np.asarray(sb[key]), err_msg=key)
+
+
+def test_fused_cull_path_in_a_device_group(icp):
+    """The multi-rank path (members of an in-process group, host gather): each member decides the
+    band and the pair shift in k_finalize_moments; the cull is still the fused one (path 1) from the
+    second iterate on, with the single-context statistics to the merge order."""
+    tgt, src, _ = icp.synth_pair(300_000, yaw_deg=2.0)
+    runs = []
+    for devices in (None, [0, 0]):
+        out = []
+        ctx = icp.Context(0) if devices is None else icp.Context(devices=devices, transport=icp.XPORT_HOST)
+        with ctx:
+            ctx.set_target(tgt, 10, 20, icp.RULES_ENGINE)
+            ctx.set_source(src)
+            T = None
+            for it in range(5):
+                st = ctx.iterate(T, it, icp.RULES_ENGINE, 3.0)
+                out.append((st.as_dict(), ctx.last_cull_path()))
+                T = icp.best_fit_from_stats(st)
+        runs.append(out)
+    for k, ((sa, pa), (sb, pb)) in enumerate(zip(*runs)):
+        assert sa["valid"] == sb["valid"]
+        np.testing.assert_allclose(sb["rmse"], sa["rmse"], rtol=1e-12)
+        np.testing.assert_allclose(sb["H"], sa["H"], rtol=1e-10, atol=1e-10 * np.abs(sa["H"]).max())
+        if k >= 2:
+            assert pa == 1 and pb == 1, (k, pa, pb)
+
+
+def _session_records(icp, tgt, src, iters, **cfg):
+    with icp.Context(0, icp.config(**cfg)) as ctx:
+        ctx.set_target(tgt, 10, 20, icp.RULES_ENGINE)
+        ctx.set_source(src)
+        rc, res, hist = ctx.run(icp.params_default(max_iterations=iters, tolerance=0.0, flags=icp.FLAG_NO_EARLY_STOP))
+        assert rc == 0
+        return [(h.valid_points, h.rmse, h.mean, h.std, h.threshold, tuple(h.transform)) for h in hist]
+
+
+def test_fused_cull_in_the_device_loop(icp):
+    """The device-resident loop takes the fused cull too (its last level is k_merge_cov_last, the
+    fused launch's fold order): its records equal the host loop's bit for bit, and the full pass
+    (fused_cull 0) to the summation order."""
+    tgt, src, _ = icp.synth_pair(400_000, yaw_deg=2.0)
+    host = _session_records(icp, tgt, src, 8, device_loop=0)
+    dev = _session_records(icp, tgt, src, 8, device_loop=1)
+    full = _session_records(icp, tgt, src, 8, device_loop=1, fused_cull=0)
+    assert host == dev
+    for (va, ra, *_), (vb, rb, *_) in zip(dev, full):
+        assert va == vb
+        np.testing.assert_allclose(ra, rb, rtol=1e-12)
+
+
+def test_fused_tail_handoff_repeated(icp):
+    """The fused last levels hand their blocks' parts to the last-arriving block with relaxed
+    agent-scope atomics and write-through stores (reduce_kernels.hip publish_part_last). A stale
+    part would change a record: 60 iterates on a 2M source (489 moment parts, fused; its cull
+    blocks fused), run twice, give the same records bit for bit, and the device loop (the cull's
+    separate last-level launch) gives them too."""
+    tgt, src, _ = icp.synth_pair(2_000_000, yaw_deg=2.0)
+    a = _session_records(icp, tgt, src, 60)
+    b = _session_records(icp, tgt, src, 60)
+    c = _session_records(icp, tgt, src, 60, device_loop=1)
+    assert len(a) == 60 and a == b and a == c

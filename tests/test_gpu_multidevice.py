@@ -213,3 +213,95 @@ def test_cli_binary_devices_flag(icp, pair, tmp_path):
     assert "devices: 2 GPUs" in outs["two"][0] and "devices:" not in outs["one"][0]
     # same report shape (one block per cumulative transform)
     assert len(outs["one"][1].splitlines()) == len(outs["two"][1].splitlines())
+
+
+def test_comm_abort_device_loop(icp, pair):
+    """After icp_hip_comm_abort, the device-resident loop (config.device_loop = 1) fails with ERCCL
+    too, instead of registering on as a world of one with the local shard's statistics."""
+    tgt, src = pair
+    with icp.Context(0, icp.config(device_loop=1)) as ctx:
+        ctx.set_target(tgt, 10, 20, icp.RULES_ENGINE)
+        ctx.set_source(src)
+        ctx.comm_init(1, 0, icp.Context.unique_id())
+        p = icp.params_default(max_iterations=8, tolerance=0.0, flags=icp.FLAG_NO_EARLY_STOP)
+        s = ctx.session(p)
+        assert s.step_n(3) == 3
+        s.close()
+        ctx.comm_abort()
+        s = ctx.session(p)
+        with pytest.raises(icp.IcpError) as e:
+            s.step_n(3)
+        assert e.value.code == icp.ERCCL
+        s.close()
+
+
+def test_host_exchange_deadline(icp, pair):
+    """A host-exchange peer that stalls past config.peer_timeout_ms: the iterate returns EEXCHANGE
+    in bounded time, later iterates fail with ERCCL until comm_init_host, which waits for the
+    stalled callback and restores the path; the context then destroys cleanly (icp_hip.h,
+    icp_hip_comm_abort's notes)."""
+    import time
+    tgt, src = pair
+    stall = {"s": 0.0}
+
+    def exchange(local):
+        if stall["s"] > 0:
+            time.sleep(stall["s"])
+        return np.stack([local, local])  # a world of two whose peer mirrors this rank
+
+    with icp.Context(0, icp.config(peer_timeout_ms=300)) as ctx:
+        ctx.set_target(tgt, 10, 20, icp.RULES_ENGINE)
+        ctx.set_source(src)
+        ctx.comm_init_host(2, 0, exchange)
+        a = ctx.iterate(None, 0, icp.RULES_ENGINE, 3.0)
+        assert a.n == 2 * src.shape[0]
+        stall["s"] = 2.0
+        t0 = time.perf_counter()
+        with pytest.raises(icp.IcpError) as e:
+            ctx.iterate(None, 0, icp.RULES_ENGINE, 3.0)
+        assert e.value.code == icp.EEXCHANGE and "peer_timeout_ms" in str(e.value)
+        assert time.perf_counter() - t0 < 1.5
+        with pytest.raises(icp.IcpError) as e:
+            ctx.iterate(None, 0, icp.RULES_ENGINE, 3.0)
+        assert e.value.code == icp.ERCCL
+        stall["s"] = 0.0
+        t0 = time.perf_counter()
+        ctx.comm_init_host(2, 0, exchange)  # joins the exchange thread once the stalled call returns
+        assert time.perf_counter() - t0 < 10.0
+        ctx.set_source(src)
+        b = ctx.iterate(None, 0, icp.RULES_ENGINE, 3.0)
+        assert (a.valid, a.rmse) == (b.valid, b.rmse)
+        stall["s"] = 1.0
+        with pytest.raises(icp.IcpError):
+            ctx.iterate(None, 0, icp.RULES_ENGINE, 3.0)
+        t0 = time.perf_counter()
+    # destroy waits for the callback still sleeping on the exchange thread
+    assert time.perf_counter() - t0 < 10.0
+
+
+def test_rccl_deadline_aborts_and_recovers(icp):
+    """config.peer_timeout_ms over an RCCL communicator: an iterate that outlasts it (a 1 ms
+    deadline on the first iterate of a 5M source, ~2 ms of device time) is abandoned with
+    ncclCommAbort and ERCCL in bounded time; comm_init restores the multi-rank path."""
+    import time
+    tgt, src, _ = icp.synth_pair(5_000_000)
+    with icp.Context(0, icp.config(peer_timeout_ms=1)) as ctx:
+        ctx.set_target(tgt, 10, 20, icp.RULES_ENGINE)
+        ctx.set_source(src)
+        ctx.synchronize()
+        ctx.comm_init(1, 0, icp.Context.unique_id())
+        t0 = time.perf_counter()
+        with pytest.raises(icp.IcpError) as e:
+            ctx.iterate(None, 0, icp.RULES_ENGINE, 3.0)
+        assert e.value.code == icp.ERCCL and "peer_timeout_ms" in str(e.value)
+        assert time.perf_counter() - t0 < 5.0
+        with pytest.raises(icp.IcpError) as e:
+            ctx.iterate(None, 0, icp.RULES_ENGINE, 3.0)
+        assert e.value.code == icp.ERCCL
+        ctx.comm_init(1, 0, icp.Context.unique_id())
+    with icp.Context(0, icp.config(peer_timeout_ms=60000)) as ctx:
+        ctx.set_target(tgt, 10, 20, icp.RULES_ENGINE)
+        ctx.set_source(src)
+        ctx.comm_init(1, 0, icp.Context.unique_id())
+        st = ctx.iterate(None, 0, icp.RULES_ENGINE, 3.0)
+        assert st.n == src.shape[0]

@@ -77,6 +77,18 @@ def main():
     if "TCC_HIT_sum" in hits and "TCC_MISS_sum" in hits:
         h, m = hits["TCC_HIT_sum"][0], hits["TCC_MISS_sum"][0]
         out["l2_hit_rate"] = h / (h + m) if h + m else None
+    sq = per_dispatch(prof, "pmc_sq")
+    if "SQ_WAVES" in sq and "SQ_INSTS_VALU" in sq and "GRBM_GUI_ACTIVE" in sq:
+        waves = sq["SQ_WAVES"][0]
+        cyc = sq["GRBM_GUI_ACTIVE"][0] / 8  # GRBM_GUI_ACTIVE sums the 8 XCDs
+        out["sq"] = {k: v[0] for k, v in sorted(sq.items())}
+        out["valu_per_wave"] = sq["SQ_INSTS_VALU"][0] / waves
+        out["salu_per_wave"] = sq["SQ_INSTS_SALU"][0] / waves if "SQ_INSTS_SALU" in sq else None
+        out["kernel_cycles"] = cyc
+        # a wave64 VALU instruction occupies its SIMD (16 lanes wide) 4 cycles; 256 CUs x 4 SIMDs
+        out["valu_issue_frac"] = sq["SQ_INSTS_VALU"][0] * 4 / (1024 * cyc)
+        if "SQ_ACTIVE_INST_VALU" in sq:
+            out["valu_active_frac"] = sq["SQ_ACTIVE_INST_VALU"][0] * 4 / (1024 * cyc)
     print(json.dumps(out, indent=1))
 
 

@@ -21,6 +21,10 @@ timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_wr
   python3 $BENCH --steps $STEPS --warmup $WARMUP > /dev/null 2> "$OUT/pmc_write.err" || exit $?
 timeout -k 10 600 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv -d "$OUT/pmc_l2" -o "$TAG" -- \
   python3 $BENCH --steps $STEPS --warmup $WARMUP > /dev/null 2> "$OUT/pmc_l2.err" || exit $?
+# the VALU / SALU issue of the search kernel (the bound that binds it: SQ_INSTS_VALU x 4 cycles per
+# wave64 instruction over 1024 SIMDs x the kernel's cycles)
+timeout -k 10 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pmc_sq" -o "$TAG" -- \
+  python3 $BENCH --steps $STEPS --warmup $WARMUP > /dev/null 2> "$OUT/pmc_sq.err" || exit $?
 cd "$REPO"
 python3 tools/pmc_traffic.py "$OUT" "$N" 1 > "$OUT/traffic.json"
 cat "$OUT/traffic.json"
