@@ -411,7 +411,7 @@ def main() -> int:
     nn_avg_s = float(np.mean(nn_ms)) / 1e3
     need = compulsory_bytes(n_local, n, n, info["n_nodes"])
     achieved = need / nn_avg_s / 1e9
-    traffic = None
+    traffic = valu = None
     tj = Path(args.traffic_json)
     if tj.exists():
         try:
@@ -419,8 +419,20 @@ def main() -> int:
             # only a profile of this exact kernel source and workload counts
             if tr.get("n") == n and tr.get("world") == shards and tr.get("search_src_sha1") == search_source_sha1():
                 traffic = tr.get("bytes_per_launch")
+                if tr.get("valu_issue_frac") is not None:
+                    # the bound that binds the search kernel: VALU issue (SQ counters of the same
+                    # profile): SQ_INSTS_VALU x 4 cycles per wave64 instruction on a 16-lane SIMD
+                    # over 1024 SIMDs x the kernel's cycles (GRBM_GUI_ACTIVE / 8 XCDs)
+                    valu = {"insts_per_wave": round(tr["valu_per_wave"], 1),
+                            "salu_per_wave": None if tr.get("salu_per_wave") is None else round(tr["salu_per_wave"], 1),
+                            "issue_frac": round(tr["valu_issue_frac"], 4),
+                            "active_frac": None if tr.get("valu_active_frac") is None else round(tr["valu_active_frac"], 4),
+                            "kernel_cycles": round(tr["kernel_cycles"]),
+                            "peak": "1 wave64 VALU instruction per 4 cycles per SIMD, 1024 SIMDs",
+                            "source": "rocprofv3 --pmc SQ_* of this kernel source, the driver's window "
+                                      "(profiles/traffic_latest.json)"}
         except Exception:
-            traffic = None
+            traffic = valu = None
 
     value = n * args.steps / elapsed / 1e6
 
@@ -488,6 +500,8 @@ def main() -> int:
             "roofline": None if shared_gpu else {
                 "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "valu": valu,
+                "binding": None if valu is None else ("valu" if valu["issue_frac"] > achieved / HBM_PEAK_GBS else "hbm"),
                 "traffic_over_algorithmic": None if traffic is None else round(traffic / need, 3),
                 # the PMC bytes of the same launch over this run's kernel time: L2 -> fabric
                 # requests, which include Infinity-Cache (MALL) hits, so an upper bound of the HBM

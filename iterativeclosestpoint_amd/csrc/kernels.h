@@ -58,12 +58,18 @@ static_assert(sizeof(WaveStat) == 160, "WaveStat is 20 doubles");
 // The entries are the points inside B+ as fp32 offsets from B+'s centre (the scan's own staging
 // values) with the point's id in the fourth word: a reusing wave streams them, no gathers.
 constexpr int kWaveCandCap = 1008;  // candidate points per wave (the walk's list in LDS; the cache)
+// One wave's candidate-cache record: its stored box B+ (the scan frame is B+'s centre), the count
+// of entries, the generation, and vmin = vol(B+) / candidate_loose (the loose test: reused only
+// while vol(B) >= vmin). One 64-B line, loaded by lanes 0..7 of the wave with its query.
 struct WaveBox {
   double lo[3];
   double hi[3];
   int32_t count;
   uint32_t gen;
+  float vmin;
+  uint32_t pad;
 };
+static_assert(sizeof(WaveBox) == 64, "one line, eight words");
 
 struct NNLaunch {
   const LoopDev* loop;      // device loop (null: the host drives the iterate); T from loop->core.T

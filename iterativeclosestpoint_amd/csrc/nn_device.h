@@ -263,6 +263,23 @@ __device__ __forceinline__ void load_query(const NNLaunch& a, int64_t i, bool ac
   }
 }
 
+// The iterate's transform (the device loop's pending increment, or the launch's), read with scalar
+// loads into scalar registers: one pointer select between the kernel argument and global memory
+// made it a generic pointer, loaded by flat loads into 24 vector registers (spills in the wave
+// search). The device loop's T was written by an earlier kernel of the stream: the scalar cache
+// holds nothing of it (it is invalidated at every dispatch) and nothing writes it meanwhile.
+typedef const __attribute__((address_space(4))) double* const_dptr;
+__device__ __forceinline__ void load_T(const NNLaunch& a, double (&T)[12]) {
+  if (a.loop) {
+    const_dptr p = (const_dptr)(a.loop->core.T);
+#pragma unroll
+    for (int k = 0; k < 12; k++) T[k] = p[k];
+  } else {
+#pragma unroll
+    for (int k = 0; k < 12; k++) T[k] = a.T[k];
+  }
+}
+
 // load_query for a 32-bit index (qat addressing; the wave search), WITHOUT the store of the moved
 // query: the wave search stores it with its results (store_query32), so that no store is pending
 // while its first loads are waited for.
@@ -274,7 +291,8 @@ __device__ __forceinline__ void load_query32(const NNLaunch& a, int32_t i, bool 
   qy = qat(a.y, i);
   qz = qat(a.z, i);
   if (APPLY) {
-    const double* T = a.loop ? a.loop->core.T : a.T;  // the device loop's pending increment
+    double T[12];
+    load_T(a, T);
     const double nx = ((T[0] * qx + T[1] * qy) + T[2] * qz) + T[3];
     const double ny = ((T[4] * qx + T[5] * qy) + T[6] * qz) + T[7];
     const double nz = ((T[8] * qx + T[9] * qy) + T[10] * qz) + T[11];

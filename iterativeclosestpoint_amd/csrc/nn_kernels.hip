@@ -112,9 +112,11 @@ static_assert(kWaveQueue * 4 + kWavePoints * 4 >= 128 * 16, "a reusing wave stag
 // fp32 radius r >= sqrt(u) (1 + 2^-40) + amax 2^-45 (the ball of the wave search's certificate):
 // the fp32 square root rounded up ((float) rounds by <= 2^-24, v_sqrt_f32 is within 1 ulp, each
 // fp32 product by <= 2^-24), the amax term doubled, 2^-49 absolute for u
-// below the fp32 normal range, and the sum's rounding covered by the 2^-21 factors.
+// below the fp32 normal range (a flushed denormal input gives 0), and the sum's rounding covered
+// by the 2^-21 factors. The bare v_sqrt_f32 (__builtin_amdgcn_sqrtf), not the correctly rounded
+// sequence __builtin_sqrtf compiles to (~13 more instructions per wave).
 __device__ __forceinline__ float ball_radius32(double u, double amax) {
-  const float s = __builtin_sqrtf((float)u * (1.0f + 0x1p-21f)) * (1.0f + 0x1p-21f);
+  const float s = __builtin_amdgcn_sqrtf((float)u * (1.0f + 0x1p-21f)) * (1.0f + 0x1p-21f);
   return s + ((float)(amax * 0x1p-44) + 0x1p-49f);
 }
 
@@ -145,7 +147,7 @@ __device__ __forceinline__ double scan32_lower_bound(float s32, double ext) {
   if (!(n2 > 0.0)) return 0.0;
   // sqrt(n2) from below: (float) rounds by <= 2^-24 (scaled down first), v_sqrt_f32 is within
   // 1 ulp, the fp64 factor covers both (a flushed denormal gives 0, still a lower bound)
-  const double n = (double)__builtin_sqrtf((float)(n2 * (1.0 - 0x1p-22))) * (1.0 - 0x1p-21);
+  const double n = (double)__builtin_amdgcn_sqrtf((float)(n2 * (1.0 - 0x1p-22))) * (1.0 - 0x1p-21);
   const double d = (n - e_abs) * (1.0 - u) * (1.0 - 0x1p-50);
   if (!(d > 0.0)) return 0.0;
   return d * d * (1.0 - 0x1p-48);
@@ -235,8 +237,8 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
   double4* stage = reinterpret_cast<double4*>(wl);  // after the walk only
   int32_t* plist = queue + kWaveQueue;               // candidate points
 
-  // The first round trip: the query, its previous match (leaf order), the wave's cache record (7
-  // words on lanes 0..6) and its first 64 entries, all issued before any of them is used (a
+  // The first round trip: the query, its previous match (leaf order), the wave's cache record (8
+  // words on lanes 0..7) and its first 64 entries, all issued before any of them is used (a
   // reusing wave has its first chunk before the box is known; unused otherwise).
   const int32_t i0 = __builtin_amdgcn_readfirstlane(i);
   const uint32_t wid = (uint32_t)i0 >> 6;
@@ -247,7 +249,7 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
   double hdr = 0.0;
   float4 ent0 = make_float4(0.f, 0.f, 0.f, 0.f);
   if (use_wc) {
-    if (lane < 7) hdr = reinterpret_cast<const double*>(a.wc_box + wid)[lane];
+    if (lane < 8) hdr = reinterpret_cast<const double*>(a.wc_box + wid)[lane];
     ent0 = a.wc_ents[(size_t)wid * kWaveCandCap + lane];
   }
   double qx = 0.0, qy = 0.0, qz = 0.0;
@@ -382,8 +384,6 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
   PCLK(t_p1);
   // Phase 2: the wave's search box over the lanes that join. Every point with fl(d2) <= u (1 +
   // 2^-47) lies within r of the query, r >= sqrt(u) (1 + 2^-40) + |q|_max 2^-45 (ball_radius32).
-  // B may be any box that holds the joined balls: it is reduced in fp32 relative to the first
-  // joined query o, rounded outwards, and converted back to fp64 rounded outwards.
   const double amax = __builtin_fmax(__builtin_fabs(qx), __builtin_fmax(__builtin_fabs(qy), __builtin_fabs(qz)));
   // |q| <= 2^100 keeps every fp32 offset of the wave finite
   const bool cand = active && finite_q && !safe && u <= 0x1p900 && amax <= 0x1p100;
@@ -392,67 +392,106 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
   // the join rule is a heuristic (any subset may join): fp32 mean
   const float mean_r = wave_sum_f(r) * __builtin_amdgcn_rcpf((float)(cmask ? __popcll(cmask) : 1));
   bool join = cand && r <= (float)a.join_factor * mean_r;
-  // The scan groups (NG kd sub-buckets of 64 / NG lanes) get their own boxes, over their own
-  // joined lanes, from the same reductions (row / half partial results on the way).
-  double blx = 0.0, bly = 0.0, blz = 0.0, bhx = -1.0, bhy = -1.0, bhz = -1.0;
+  const unsigned long long jm = __ballot(join);
+
+  // The frame of the box reductions: fp32 offsets from an origin o. A wave whose cache record is of
+  // this generation takes o = the centre of its stored B+, the frame its entries were stored in: a
+  // reusing wave then gets its search box (for the reuse test), its scan groups' boxes and its
+  // queries' scan offsets out of one reduction, in the frame it scans in, with no fp64 box and no
+  // conversion of the group boxes (which cost ~290 VALU instructions per wave, most of them on
+  // wave-uniform values). Any other wave takes o = its first joined query and, once its frame is
+  // known (after its walk), reduces again in that frame.
+  const bool have_rec =
+      use_wc && jm != 0 &&
+      (uint32_t)__builtin_amdgcn_readlane((int)((unsigned long long)__double_as_longlong(hdr) >> 32), 6) == a.wc_gen;
   double ox_ = 0.0, oy_ = 0.0, oz_ = 0.0;
-  float glo[NG][3], ghi[NG][3];  // group boxes relative to o (wave-uniform); empty: +inf / -inf
-  {
-    const unsigned long long jm = __ballot(join);
-    if (jm != 0) {
-      const int ol = __builtin_ctzll(jm);
-      ox_ = readlane_d(qx, ol);
-      oy_ = readlane_d(qy, ol);
-      oz_ = readlane_d(qz, ol);
-      const double dq[3] = {qx - ox_, qy - oy_, qz - oz_};
-      float wlo[3], whi[3];
+  int pkl[3] = {0, 0, 0}, pkh[3] = {0, 0, 0};  // B+ - o rounded inwards (fp32 keys; have_rec)
+  float pext = 0.f;                            // max |B+ - o| (1 + 2^-22) >= that of every point in B+
+  if (have_rec) {
+    // lanes 0..5 hold B+'s bounds (lo x, y, z, hi x, y, z): lanes j and j + 3 form axis j's centre,
+    // the same operation as the store's (lo + hi) * 0.5 (the sum commutes exactly)
+    const double part = __shfl(hdr, lane < 3 ? lane + 3 : (lane < 6 ? lane - 3 : lane), kWave);
+    const double c = (hdr + part) * 0.5;
+    ox_ = readlane_d(c, 0);
+    oy_ = readlane_d(c, 1);
+    oz_ = readlane_d(c, 2);
+    // the bounds relative to o, in fp32 rounded inwards (the conversion rounds by <= 2^-24
+    // relative, the fma moves the bound inwards by |f| 2^-22): containment in them is containment
+    // in B+
+    const float f = (float)(hdr - c);
+    const int key = fkey(__builtin_fmaf(__builtin_fabsf(f), lane < 3 ? 0x1p-22f : -0x1p-22f, f));
 #pragma unroll
-      for (int k = 0; k < 3; k++) {
-        const float d = (float)dq[k];
-        const float m = (__builtin_fabsf(d) + r) * 0x1p-21f + 0x1p-126f;
-        int kl = fkey(join ? (d - r) - m : __builtin_inff());
-        int kh = fkey(join ? (d + r) + m : -__builtin_inff());
-        kl = rows_min_i(kl);
-        kh = rows_max_i(kh);
-        if (NG == 4) {
-#pragma unroll
-          for (int g = 0; g < 4; g++) {
-            glo[g][k] = funkey(__builtin_amdgcn_readlane(kl, 16 * g + 15));
-            ghi[g][k] = funkey(__builtin_amdgcn_readlane(kh, 16 * g + 15));
-          }
-        }
-        kl = halves_min_i(kl);
-        kh = halves_max_i(kh);
-        if (NG == 2) {
-#pragma unroll
-          for (int g = 0; g < 2; g++) {
-            glo[g][k] = funkey(__builtin_amdgcn_readlane(kl, 32 * g + 31));
-            ghi[g][k] = funkey(__builtin_amdgcn_readlane(kh, 32 * g + 31));
-          }
-        }
-        wlo[k] = funkey(__builtin_amdgcn_readlane(wave_min_from_halves(kl), 63));
-        whi[k] = funkey(__builtin_amdgcn_readlane(wave_max_from_halves(kh), 63));
-        if (NG == 1) {
-          glo[0][k] = wlo[k];
-          ghi[0][k] = whi[k];
-        }
-      }
-      blx = uniform_d(box_lo(ox_, wlo[0]));
-      bly = uniform_d(box_lo(oy_, wlo[1]));
-      blz = uniform_d(box_lo(oz_, wlo[2]));
-      bhx = uniform_d(box_hi(ox_, whi[0]));
-      bhy = uniform_d(box_hi(oy_, whi[1]));
-      bhz = uniform_d(box_hi(oz_, whi[2]));
-    } else {
-#pragma unroll
-      for (int g = 0; g < NG; g++)
-#pragma unroll
-        for (int k = 0; k < 3; k++) {
-          glo[g][k] = __builtin_inff();
-          ghi[g][k] = -__builtin_inff();
-        }
+    for (int k = 0; k < 3; k++) {
+      pkl[k] = __builtin_amdgcn_readlane(key, k);
+      pkh[k] = __builtin_amdgcn_readlane(key, k + 3);
     }
+    // max over lanes 0..5 of |f| (row_shr 1, 2, 4: lane 5 sees lanes 0..5)
+    int e = lane < 6 ? __float_as_int(__builtin_fabsf(f)) : 0;
+    e = max(e, __builtin_amdgcn_update_dpp(0, e, 0x111, 0xf, 0xf, false));
+    e = max(e, __builtin_amdgcn_update_dpp(0, e, 0x112, 0xf, 0xf, false));
+    e = max(e, __builtin_amdgcn_update_dpp(0, e, 0x114, 0xf, 0xf, false));
+    pext = __int_as_float(__builtin_amdgcn_readlane(e, 5)) * (1.0f + 0x1p-21f);
+  } else if (jm != 0) {
+    const int ol = __builtin_ctzll(jm);
+    ox_ = readlane_d(qx, ol);
+    oy_ = readlane_d(qy, ol);
+    oz_ = readlane_d(qz, ol);
   }
+  // The reductions: per axis, the joined balls' bounds in fp32 offsets from o, rounded outwards
+  // (m covers the conversion of q - o and the roundings of the two sums), reduced with integer
+  // DPP min/max on order-preserving keys: the scan groups' boxes (NG kd sub-buckets of 64 / NG
+  // lanes) at their rows' / halves' last lanes, the wave's box (B) as scalar keys.
+  int gkl[3], gkh[3];  // group-level keys: lane 16 g + 15 (NG 4), 32 g + 31 (NG 2), 63 (NG 1)
+  int wkl[3], wkh[3];  // the wave's box B - o (scalar)
+  auto reduce = [&](float d0, float d1, float d2) {
+    const float dd[3] = {d0, d1, d2};
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      const float d = dd[k];
+      const float m = (__builtin_fabsf(d) + r) * 0x1p-21f + 0x1p-126f;
+      int kl = fkey(join ? (d - r) - m : __builtin_inff());
+      int kh = fkey(join ? (d + r) + m : -__builtin_inff());
+      kl = rows_min_i(kl);
+      kh = rows_max_i(kh);
+      if (NG == 4) {
+        gkl[k] = kl;
+        gkh[k] = kh;
+      }
+      kl = halves_min_i(kl);
+      kh = halves_max_i(kh);
+      if (NG == 2) {
+        gkl[k] = kl;
+        gkh[k] = kh;
+      }
+      kl = wave_min_from_halves(kl);
+      kh = wave_max_from_halves(kh);
+      if (NG == 1) {
+        gkl[k] = kl;
+        gkh[k] = kh;
+      }
+      wkl[k] = __builtin_amdgcn_readlane(kl, 63);
+      wkh[k] = __builtin_amdgcn_readlane(kh, 63);
+    }
+  };
+  // Group boxes in the scan frame, widened by mg >= ext 2^-20: a point of a joined lane's ball is
+  // staged for the lane's group whatever the fp32 rounding of its offset (<= ext 2^-24). Widened on
+  // the group lanes, then read into scalar registers (an empty group: +inf / -inf).
+  float gl[NG][3], gh[NG][3];
+  auto group_bounds = [&](float mg) {
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      const float lo = funkey(gkl[k]) - mg, hi = funkey(gkh[k]) + mg;
+#pragma unroll
+      for (int g = 0; g < NG; g++) {
+        gl[g][k] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(lo), (64 / NG) * g + 64 / NG - 1));
+        gh[g][k] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(hi), (64 / NG) * g + 64 / NG - 1));
+      }
+    }
+  };
+  if (jm != 0) reduce((float)(qx - ox_), (float)(qy - oy_), (float)(qz - oz_));
+  // a wave with a record takes its group boxes in the record's frame right away (the reduction's
+  // vector registers die here; a wave that then walks reduces again in its new frame)
+  if (have_rec) group_bounds(pext * 0x1p-20f);
 
   PCLK(t_p2);
   // Phase 3: the leaves meeting B. With the candidate cache (iterate only), a walk collects the
@@ -552,59 +591,46 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
   };
   bool wstore = false, reuse = false;
   double wlx = 0.0, wly = 0.0, wlz = 0.0, whx = 0.0, why = 0.0, whz = 0.0;  // B+ of a walk
-  // the frame box: its centre is the scan's origin (B+ with the cache, else B)
-  double flx = blx, fly = bly, flz = blz, fhx = bhx, fhy = bhy, fhz = bhz;
+  double blx = 0.0, bly = 0.0, blz = 0.0, bhx = -1.0, bhy = -1.0, bhz = -1.0;  // B (fp64) of a walking wave
+  double ocx = ox_, ocy = oy_, ocz = oz_;  // the scan frame's centre (B+'s with the cache, else B's)
+  double ext = 0.0;  // >= |offset| of every point inside B and every joined query, in the frame
   WaveBox* wb = nullptr;
   float4* wents = nullptr;
-  if (__ballot(join) != 0) {
+  if (jm != 0) {
     if (use_wc) {
       wb = a.wc_box + wid;
       wents = a.wc_ents + (size_t)wid * kWaveCandCap;
-      const double hlx = readlane_d(hdr, 0), hly = readlane_d(hdr, 1), hlz = readlane_d(hdr, 2);
-      const double hhx = readlane_d(hdr, 3), hhy = readlane_d(hdr, 4), hhz = readlane_d(hdr, 5);
-      const unsigned long long cg = (unsigned long long)__double_as_longlong(readlane_d(hdr, 6));
-      // reused while B lies inside B+ and B+ is not much larger than B (a wave whose box shrank,
-      // e.g. after the first iterate's descent guesses, walks again and stores a tighter list)
-      reuse = (uint32_t)(cg >> 32) == a.wc_gen && blx >= hlx && bly >= hly && blz >= hlz && bhx <= hhx &&
-              bhy <= hhy && bhz <= hhz &&
-              (hhx - hlx) * (hhy - hly) * (hhz - hlz) <= a.wc_loose * ((bhx - blx) * (bhy - bly) * (bhz - blz));
-      if (kDbg && a.dbg && lane == 0 && !reuse && (uint32_t)(cg >> 32) == a.wc_gen) {
-        const bool inside = blx >= hlx && bly >= hly && blz >= hlz && bhx <= hhx && bhy <= hhy && bhz <= hhz;
-        atomicAdd(&a.dbg[inside ? 25 : 24], 1ull);
-        if (!inside && APPLY) {
-          // which side B left B+ by, against this iterate's motion of B's centre: the side it
-          // moves to (27) or the opposite side (28); and whether B is larger than B+ on an axis
-          // (29: its balls grew past the margins)
-          const double* T = a.loop ? a.loop->core.T : a.T;
-          const double c[3] = {(blx + bhx) * 0.5, (bly + bhy) * 0.5, (blz + bhz) * 0.5};
-          const double lo[3] = {blx, bly, blz}, hi[3] = {bhx, bhy, bhz}, plo[3] = {hlx, hly, hlz}, phi[3] = {hhx, hhy, hhz};
-          bool fwd = false, back = false, grew = false;
-          for (int k = 0; k < 3; k++) {
-            const double e = (((T[4 * k] * c[0] + T[4 * k + 1] * c[1]) + T[4 * k + 2] * c[2]) + T[4 * k + 3]) - c[k];
-            if (lo[k] < plo[k]) (e < 0.0 ? fwd : back) = true;
-            if (hi[k] > phi[k]) (e > 0.0 ? fwd : back) = true;
-            grew = grew || (hi[k] - lo[k]) > (phi[k] - plo[k]);
-          }
-          if (fwd) atomicAdd(&a.dbg[27], 1ull);
-          if (back) atomicAdd(&a.dbg[28], 1ull);
-          if (grew) atomicAdd(&a.dbg[29], 1ull);
-        }
-      }
-      if (reuse) {
-        nleaf = (int)(uint32_t)cg;
-        flx = hlx;
-        fly = hly;
-        flz = hlz;
-        fhx = hhx;
-        fhy = hhy;
-        fhz = hhz;
-        if (kDbg && a.dbg && lane == 0) {
-          atomicAdd(&a.dbg[12], 1ull);
-          atomicAdd(&a.dbg[17], (unsigned long long)nleaf);  // entries a reusing wave streams
-        }
-      }
     }
-    if (!reuse) {
+    if (have_rec) {
+      // reused while B lies inside B+ (exact: B's fp32 bounds are rounded outwards, B+'s inwards)
+      // and B+ is not much larger than B (vol(B) >= the record's vmin = vol(B+) / wc_loose: a wave
+      // whose box shrank, e.g. after the first iterate's descent guesses, walks again and stores a
+      // tighter list)
+      bool inside = true;
+#pragma unroll
+      for (int k = 0; k < 3; k++) inside = inside && wkl[k] >= pkl[k] && wkh[k] <= pkh[k];
+      const float vb = (funkey(wkh[0]) - funkey(wkl[0])) * (funkey(wkh[1]) - funkey(wkl[1])) *
+                       (funkey(wkh[2]) - funkey(wkl[2]));
+      const float vmin = __int_as_float(__builtin_amdgcn_readlane((int)(unsigned)__double_as_longlong(hdr), 7));
+      reuse = inside && vb >= vmin;
+      if (kDbg && a.dbg && lane == 0 && !reuse) atomicAdd(&a.dbg[inside ? 25 : 24], 1ull);
+    }
+    if (reuse) {
+      nleaf = __builtin_amdgcn_readlane((int)(unsigned)__double_as_longlong(hdr), 6);
+      // the frame is o: the reduction's offsets are the scan's, its group boxes the scan's
+      ext = (double)pext * (1.0 + 0x1p-20);
+      if (kDbg && a.dbg && lane == 0) {
+        atomicAdd(&a.dbg[12], 1ull);
+        atomicAdd(&a.dbg[17], (unsigned long long)nleaf);  // entries a reusing wave streams
+      }
+    } else {
+      // B in fp64: o + the wave's bounds, rounded outwards
+      blx = uniform_d(box_lo(ox_, funkey(wkl[0])));
+      bly = uniform_d(box_lo(oy_, funkey(wkl[1])));
+      blz = uniform_d(box_lo(oz_, funkey(wkl[2])));
+      bhx = uniform_d(box_hi(ox_, funkey(wkh[0])));
+      bhy = uniform_d(box_hi(oy_, funkey(wkh[1])));
+      bhz = uniform_d(box_hi(oz_, funkey(wkh[2])));
       // B+ (B itself without the cache); an overflowing B+ makes an overflowing wave (its lanes
       // take the ball search; ~0.06 % of the waves at 10M with the default margin). Wave-uniform
       // doubles are kept in scalar registers.
@@ -619,7 +645,8 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
       // record lasts against how many entries a reusing wave streams.
       double dlx = 0.0, dly = 0.0, dlz = 0.0, dhx = 0.0, dhy = 0.0, dhz = 0.0;
       if (APPLY && keep && a.wc_lead > 0.0) {
-        const double* T = a.loop ? a.loop->core.T : a.T;
+        double T[12];
+        load_T(a, T);
         const double cx = (blx + bhx) * 0.5, cy = (bly + bhy) * 0.5, cz = (blz + bhz) * 0.5;
         const double ex = (((T[0] * cx + T[1] * cy) + T[2] * cz) + T[3]) - cx;
         const double ey = (((T[4] * cx + T[5] * cy) + T[6] * cz) + T[7]) - cy;
@@ -656,17 +683,30 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
         walk(wlx, wly, wlz, whx, why, whz);
       }
       wstore = keep && !overflow;
+      // the frame: B+'s centre with the cache (the stored record's), else B's
       if (keep) {
-        flx = wlx;
-        fly = wly;
-        flz = wlz;
-        fhx = whx;
-        fhy = why;
-        fhz = whz;
+        ocx = (wlx + whx) * 0.5;
+        ocy = (wly + why) * 0.5;
+        ocz = (wlz + whz) * 0.5;
+      } else {
+        ocx = (blx + bhx) * 0.5;
+        ocy = (bly + bhy) * 0.5;
+        ocz = (blz + bhz) * 0.5;
+      }
+      ocx = uniform_d(ocx);
+      ocy = uniform_d(ocy);
+      ocz = uniform_d(ocz);
+      // |offset| <= ext for every point inside B and every joined query (B lies in the frame box)
+      ext = dmax_(dmax_(dmax_(bhx - ocx, ocx - blx), dmax_(bhy - ocy, ocy - bly)), dmax_(bhz - ocz, ocz - blz)) *
+            (1.0 + 0x1p-40);
+      if (!overflow && nleaf > 0) {
+        // the group boxes and the queries' offsets again, in the frame
+        reduce((float)(qx - ocx), (float)(qy - ocy), (float)(qz - ocz));
+        group_bounds((float)(ext * 0x1p-20));
       }
     }
   }
-  // the cache record of a stored list (entries already written)
+  // the cache record of a stored list (entries already written); vmin: the loose test's bound
   auto store_header = [&](int count) {
     if (lane == 0) {
       wb->lo[0] = wlx;
@@ -677,6 +717,7 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
       wb->hi[2] = whz;
       wb->count = count;
       wb->gen = a.wc_gen;
+      wb->vmin = (float)((whx - wlx) * (why - wly) * (whz - wlz) / a.wc_loose);
     }
     if (kDbg && a.dbg && lane == 0) atomicAdd(&a.dbg[13], 1ull);
   };
@@ -720,30 +761,8 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
   const int npts = nleaf;
   int scanned_pts = 0;
   bool need64 = __ballot(join) != 0 && npts > 0;
-  const double ocx = (flx + fhx) * 0.5, ocy = (fly + fhy) * 0.5, ocz = (flz + fhz) * 0.5;  // scan frame
   if (a.scan32 && need64) {
-    // |offset| <= ext for every point inside B and every joined query (B lies in the frame box)
-    const double ext = dmax_(dmax_(dmax_(bhx - ocx, ocx - blx), dmax_(bhy - ocy, ocy - bly)),
-                             dmax_(bhz - ocz, ocz - blz)) * (1.0 + 0x1p-40);
     if (ext >= 0x1p-40 && ext <= 0x1p60) {
-      const float qx32 = (float)(qx - ocx), qy32 = (float)(qy - ocy), qz32 = (float)(qz - ocz);
-      // Group boxes in the scan frame, widened by ext 2^-20: a point of a joined lane's ball is
-      // staged for the lane's group whatever the fp32 rounding of its offset (<= ext 2^-24). A
-      // staged point has |offset| <= ext (1 + 2^-20) (ext_s below).
-      const float mg = (float)(ext * 0x1p-20);
-      const float dox = (float)(ox_ - ocx), doy = (float)(oy_ - ocy), doz = (float)(oz_ - ocz);
-      float gl[NG][3], gh[NG][3];
-      // wave-uniform: kept in scalar registers (readfirstlane), not in 6 NG vector registers
-      auto uni = [](float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); };
-#pragma unroll
-      for (int g = 0; g < NG; g++) {
-        gl[g][0] = uni((glo[g][0] + dox) - mg);
-        gl[g][1] = uni((glo[g][1] + doy) - mg);
-        gl[g][2] = uni((glo[g][2] + doz) - mg);
-        gh[g][0] = uni((ghi[g][0] + dox) + mg);
-        gh[g][1] = uni((ghi[g][1] + doy) + mg);
-        gh[g][2] = uni((ghi[g][2] + doz) + mg);
-      }
       constexpr int LG = 64 / NG;  // lanes of a group
       // points of a group's segment per round: LG for a walking wave (its candidate list occupies
       // the list area); a wave that reuses its cache record leaves the list area unused, so it
@@ -767,17 +786,23 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
       int32_t p1 = -1;
       typedef float f2 __attribute__((ext_vector_type(2)));
       typedef int v4i __attribute__((ext_vector_type(4)));
+      // the queries' offsets in the frame (a reusing wave's are its reduction's, bit for bit)
+      const float qx32 = (float)(qx - ocx), qy32 = (float)(qy - ocy), qz32 = (float)(qz - ocz);
       const f2 qx2 = {qx32, qx32}, qy2 = {qy32, qy32}, qz2 = {qz32, qz32};
       // ~63 in a vector register: with it (a literal cannot be a VOP3 operand on gfx9) the key is
       // one v_and_or_b32 instead of v_and_b32 + v_or_b32
       uint32_t kmask = ~63u;
       asm volatile("" : "+v"(kmask));
-      auto sel = [&](float sq, uint32_t sl) {
-        const float key = __uint_as_float((__float_as_uint(sq) & kmask) | sl);
-        k2 = __builtin_amdgcn_fmed3f(k1, k2, key);
-        // k1 = min(k1, key) as one VOP2 v_min_f32 (2/3 the issue cost of a VOP3 v_med3_f32 on
-        // gfx950; keys are never NaN, so no canonicalisation is needed)
-        asm("v_min_f32 %0, %1, %2" : "=v"(k1) : "v"(key), "v"(k1));
+      // The two smallest of {k1, k2, a, b} (k1 <= k2) in three instructions per pair of points:
+      // k1' = min3(k1, a, b); the second smallest is min(med3(k1, a, b), k2) (if k2 is below the
+      // median of the other three it is second, as k1 <= k2; otherwise the median is). Keys are
+      // never NaN, so no canonicalisation is needed; the last min is one VOP2 v_min_f32 (2/3 the
+      // issue cost of a VOP3 on gfx950).
+      auto sel2 = [&](float ka, float kb) {
+        float m;
+        asm("v_med3_f32 %0, %1, %2, %3" : "=v"(m) : "v"(k1), "v"(ka), "v"(kb));
+        asm("v_min3_f32 %0, %1, %2, %3" : "=v"(k1) : "v"(k1), "v"(ka), "v"(kb));
+        asm("v_min_f32 %0, %1, %2" : "=v"(k2) : "v"(m), "v"(k2));
       };
       auto eval2 = [&](const v4i xy, const v4i zw, uint32_t sl) {
         const f2 X = {__int_as_float(xy.x), __int_as_float(xy.y)};
@@ -785,8 +810,10 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
         const f2 Z = {__int_as_float(zw.x), __int_as_float(zw.y)};
         const f2 dx = X - qx2, dy = Y - qy2, dz = Z - qz2;
         const f2 sq = __builtin_elementwise_fma(dz, dz, __builtin_elementwise_fma(dy, dy, dx * dx));
-        sel(sq.x, sl);
-        sel(sq.y, (uint32_t)__builtin_amdgcn_readfirstlane((int)(sl + 1u)));  // a scalar operand
+        const float ka = __uint_as_float((__float_as_uint(sq.x) & kmask) | sl);
+        const float kb = __uint_as_float((__float_as_uint(sq.y) & kmask) |
+                                         (uint32_t)__builtin_amdgcn_readfirstlane((int)(sl + 1u)));  // a scalar operand
+        sel2(ka, kb);
       };
       const v4i* st4 = reinterpret_cast<const v4i*>(stage32) + 2 * blk(0, gq);  // this group's pair 0
       constexpr int kStep = 2 * NG;                                             // v4i per pair step
@@ -1014,6 +1041,17 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
     // (identical points take the same octant at every split), where the reference's strict <
     // keeps the first in leaf order, i.e. the smallest position; `second` is the smallest fl(d2)
     // of the points that are not copies of the winner (any other equal distance stays a tie).
+    // A reusing wave has no fp64 B (its reduction ran in the frame): it filters with its stored
+    // B+, which holds B (a superset is exact, only the work grows; this path is rare).
+    double xlx = blx, xly = bly, xlz = blz, xhx = bhx, xhy = bhy, xhz = bhz;
+    if (reuse) {
+      xlx = wb->lo[0];
+      xly = wb->lo[1];
+      xlz = wb->lo[2];
+      xhx = wb->hi[0];
+      xhy = wb->hi[1];
+      xhz = wb->hi[2];
+    }
     wave_lds_fence();
     double4 nxtp = make_double4(0.0, 0.0, 0.0, 0.0);
     bool nin = false;
@@ -1027,8 +1065,8 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
     }
     int wcount = 0;  // a walking wave without an fp32 pass stores its entries here
     for (int base = 0; base < npts; base += 64) {
-      nin = base + lane < npts && nxtp.x >= blx && nxtp.x <= bhx && nxtp.y >= bly && nxtp.y <= bhy &&
-            nxtp.z >= blz && nxtp.z <= bhz;
+      nin = base + lane < npts && nxtp.x >= xlx && nxtp.x <= xhx && nxtp.y >= xly && nxtp.y <= xhy &&
+            nxtp.z >= xlz && nxtp.z <= xhz;
       const unsigned long long im = __ballot(nin);
       const int slot = mask_rank(im);
       const double4 cur = nxtp;
@@ -1143,8 +1181,15 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
 #endif
 }
 
+// Waves per SIMD the wave search is compiled for (its VGPR budget: 8 -> 64, 7 -> 72, 6 -> 80).
+// 7 since r20: at 8 the frame-first setup spills (27 VGPRs, scratch reloads on the critical path:
+// search 0.71 ms); at 7 it spills 6 (0.515 ms vs 0.548 for the r19 kernel at 8, 0.524 at 6;
+// profiles/r20a/ab_waves_per_eu.txt). LDS (5 KB per wave) allows 8.
+#ifndef ICP_WAVE_WPE
+#define ICP_WAVE_WPE 7
+#endif
 template <bool APPLY, int NG, bool CERT, bool DBG>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))) k_nn_wave(NNLaunch a) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ICP_WAVE_WPE, ICP_WAVE_WPE))) k_nn_wave(NNLaunch a) {
   if (a.loop && a.loop->core.done) return;  // the device loop's session finished
   extern __shared__ __attribute__((aligned(16))) unsigned long long lds_raw[];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
