@@ -285,6 +285,9 @@ def main() -> int:
                     help="every target point repeated this many times (an exact tie for every query: the "
                          "certified search's fp64 rescan gives copies of the winner the lowest slot, "
                          "as the reference's leaf order does)")
+    ap.add_argument("--scene", action="store_true",
+                    help="a LiDAR-like scene pair (icp_synth_scene: ground + walls scanned from two poses, "
+                         "range-dependent density, 1 mm grid) instead of config 4's Gaussian blob")
     ap.add_argument("--config", action="append", default=[], metavar="KEY=VALUE",
                     help="icp_hip_config field for the context (A/B of search options), repeatable")
     ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "traffic_latest.json"),
@@ -316,7 +319,7 @@ def main() -> int:
 
     n = args.points
     t_setup = time.perf_counter()
-    tgt, src, T_true = icp.synth_pair(n)
+    tgt, src, T_true = icp.synth_scene(n) if args.scene else icp.synth_pair(n)
     if args.duplicates > 1:
         tgt = np.repeat(tgt[: n // args.duplicates + 1], args.duplicates, axis=0)[:n]
     if args.quantize > 0:
@@ -475,12 +478,15 @@ def main() -> int:
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic (icp_synth_pair: N(0, diag(5,5,1)^2) target seed 42; source = R^T(target - t) "
-                    "+ 1 mm noise, 1% outliers, shuffled, seed 43)"
+            "data": ("synthetic LiDAR-like scene (icp_synth_scene: ground + 8 walls, scanner rays uniform in "
+                     "azimuth/elevation, 2 mm range noise, 1 mm grid; source = an independent scan from a moved "
+                     "scanner, 0.2 % outliers)" if args.scene else
+                     "synthetic (icp_synth_pair: N(0, diag(5,5,1)^2) target seed 42; source = R^T(target - t) "
+                     "+ 1 mm noise, 1% outliers, shuffled, seed 43)")
                     + (f"; both clouds rounded to a {args.quantize} m grid (LAS-style)" if args.quantize > 0 else "")
                     + (f"; every target point repeated {args.duplicates}x" if args.duplicates > 1 else ""),
             "config": {
-                "workload": f"{CONFIG_NAMES.get(n, 'custom')}: {n}<->{n} synthetic pair, full ICP iteration "
+                "workload": f"{'scene' if args.scene else CONFIG_NAMES.get(n, 'custom')}: {n}<->{n} synthetic pair, full ICP iteration "
                             f"(engine rules, octree leaf 10 / depth 20), "
                             f"source sharded over {shards} rank(s) on {gpus_used} GPU(s), target octree replicated",
                 "n_target": n, "n_source": n, "ranks": shards, "ranks_per_gpu": shards // gpus_used,

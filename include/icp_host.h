@@ -69,6 +69,36 @@ void icp_synth_default(icp_synth_spec* s);
 int icp_synth_pair(const icp_synth_spec* s, int64_t n_tgt, int64_t n_src, double* tgt_xyz, double* src_xyz,
                    double T_true[16]);
 
+/* A LiDAR-like scene pair (2.5-D surfaces, the data the reference's LAS flow feeds it,
+ * lasio.cpp:7-125 / icp_registration.cpp:248-378): a terrestrial scanner at scanner_height above
+ * an undulating ground (amplitude terrain_amp) with n_walls vertical walls (facades) standing
+ * within site_radius; rays uniform in azimuth and in elevation [elev_min, elev_max] (so the point
+ * density falls with range as the scanner's does), the nearest hit within 1.5 site_radius,
+ * jittered along the beam by range_noise and rounded to `quantum` (LAS 1.2's int32 x 0.001 grid).
+ * The target is one scan in the world frame; the source an independent scan from the scanner
+ * moved by t, expressed in its own frame: source = R^T (world - t), R = Rz(yaw) Ry(pitch)
+ * Rx(roll), rounded to the grid there; outlier_fraction of its points are uniform in its bbox.
+ * T_true maps source onto target. Deterministic (counter-based streams). Returns 0 or -1. */
+typedef struct icp_scene_spec {
+  double site_radius;      /* m, default 40                                      */
+  double scanner_height;   /* m, default 1.8                                     */
+  int32_t n_walls;         /* default 8                                          */
+  double wall_height;      /* m, default 6                                       */
+  double terrain_amp;      /* m, default 0.3                                     */
+  double elev_min_deg, elev_max_deg; /* default -45, 35                          */
+  double range_noise;      /* m, default 2e-3                                    */
+  double quantum;          /* m, default 1e-3 (0: no rounding)                   */
+  double yaw_deg, pitch_deg, roll_deg; /* default 2, 0.5, -0.5                   */
+  double t[3];             /* m, default (0.3, -0.2, 0.05)                       */
+  double outlier_fraction; /* default 0.002                                      */
+  uint64_t seed_target;    /* default 7                                          */
+  uint64_t seed_source;    /* default 8                                          */
+} icp_scene_spec;
+
+void icp_scene_default(icp_scene_spec* s);
+int icp_synth_scene(const icp_scene_spec* s, int64_t n_tgt, int64_t n_src, double* tgt_xyz, double* src_xyz,
+                    double T_true[16]);
+
 #ifdef __cplusplus
 }
 #endif

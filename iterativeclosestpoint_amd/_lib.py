@@ -137,6 +137,16 @@ class SynthSpec(C.Structure):
     ]
 
 
+class SceneSpec(C.Structure):
+    _fields_ = [
+        ("site_radius", C.c_double), ("scanner_height", C.c_double), ("n_walls", C.c_int32),
+        ("wall_height", C.c_double), ("terrain_amp", C.c_double), ("elev_min_deg", C.c_double),
+        ("elev_max_deg", C.c_double), ("range_noise", C.c_double), ("quantum", C.c_double),
+        ("yaw_deg", C.c_double), ("pitch_deg", C.c_double), ("roll_deg", C.c_double), ("t", C.c_double * 3),
+        ("outlier_fraction", C.c_double), ("seed_target", C.c_uint64), ("seed_source", C.c_uint64),
+    ]
+
+
 _EXCHANGE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_double), C.c_int32, C.POINTER(C.c_double))
 
 # (name, restype, argtypes) for every exported symbol; also the list the ABI test checks
@@ -211,6 +221,8 @@ SIGNATURES = {
     "icp_synth_default": (None, [C.POINTER(SynthSpec)]),
     "icp_synth_pair": (C.c_int, [C.POINTER(SynthSpec), C.c_int64, C.c_int64, _P, _P, _P]),
     "icp_source_shard_order": (C.c_int, [_P, C.c_int64, _P]),
+    "icp_scene_default": (None, [C.POINTER(SceneSpec)]),
+    "icp_synth_scene": (C.c_int, [C.POINTER(SceneSpec), C.c_int64, C.c_int64, _P, _P, _P]),
     # icp_las.h
     "icp_las_read_header": (C.c_int, [C.c_char_p, C.c_int, C.POINTER(LasHeader)]),
     "icp_las_read": (C.c_int64, [C.c_char_p, C.c_int, C.c_int64, _P, C.POINTER(LasHeader)]),
@@ -621,6 +633,24 @@ def synth_pair(n_tgt: int, n_src: int | None = None, **overrides):
     src = np.empty((n_src, 3))
     T = np.empty(16)
     _check(lib().icp_synth_pair(C.byref(spec), n_tgt, n_src, _ptr(tgt), _ptr(src), _ptr(T)))
+    return tgt, src, T.reshape(4, 4)
+
+
+def synth_scene(n_tgt: int, n_src: int | None = None, **overrides):
+    """A LiDAR-like scene pair (icp_synth_scene, include/icp_host.h): ground + walls scanned from
+    two poses, 1 mm grid. Returns (target, source, T_true)."""
+    spec = SceneSpec()
+    lib().icp_scene_default(C.byref(spec))
+    for k, v in overrides.items():
+        if k == "t":
+            spec.t[:] = list(v)
+        else:
+            setattr(spec, k, v)
+    n_src = n_tgt if n_src is None else n_src
+    tgt = np.empty((n_tgt, 3))
+    src = np.empty((n_src, 3))
+    T = np.empty(16)
+    _check(lib().icp_synth_scene(C.byref(spec), n_tgt, n_src, _ptr(tgt), _ptr(src), _ptr(T)))
     return tgt, src, T.reshape(4, 4)
 
 

@@ -528,42 +528,36 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
         }
         if (lane == 0) queue[0] = start;
       }
-      // Every batch pops up to 128 nodes (two per lane, both loads in flight), which already meet
-      // B (tested by their parent; the start nodes by the cell box or the descent), appends the
-      // points of its leaves to the candidate list and pushes its children meeting B. Most recent
-      // first: the live set stays small.
+      // Every batch pops up to 64 nodes (one per lane), which already meet B (tested by their
+      // parent; the start nodes by the cell box or the descent), appends the points of its leaves
+      // to the candidate list and pushes its children meeting B. Most recent first: the live set
+      // stays small. (Two nodes per lane, both loads in flight, cost the kernel 16 more live
+      // vector registers through this rare path, ~3 % of the waves per iterate: spills on the
+      // common path.)
       wave_lds_fence();
       while (tail > 0) {
-        const int batch = tail < 128 ? tail : 128;
-        const int e0 = tail - batch + lane;
-        const bool has0 = lane < batch, has1 = lane + 64 < batch;
-        int32_t first0 = 0, first1 = 0;
-        uint32_t meta0 = 0, meta1 = 0, kids0 = 0, kids1 = 0;
-        // both records whole (box and topology) in one round trip; lanes without a node read the
-        // root (in bounds, ignored)
-        const NodeLoad nd0 = load_node(a.nodes + (has0 ? queue[e0] : 0));
-        const NodeLoad nd1 = load_node(a.nodes + (has1 ? queue[e0 + 64] : 0));
-        if (has0) {
-          first0 = nd0.topo.x;
-          meta0 = (uint32_t)nd0.topo.y;
-        }
-        if (has1) {
-          first1 = nd1.topo.x;
-          meta1 = (uint32_t)nd1.topo.y;
-        }
-        if (has0 && !(meta0 & kLeafBit)) kids0 = children_in_box(nd0, meta0 & 0xffu, wlx, wly, wlz, whx, why, whz);
-        if (has1 && !(meta1 & kLeafBit)) kids1 = children_in_box(nd1, meta1 & 0xffu, wlx, wly, wlz, whx, why, whz);
+        const int batch = tail < 64 ? tail : 64;
+        const bool has = lane < batch;
+        // the record's box and topology in one round trip; lanes without a node read the root
+        // (in bounds, ignored)
+        const NodeRec* nr = a.nodes + (has ? queue[tail - batch + lane] : 0);
+        NodeLoad nd;
+        nd.l01 = *reinterpret_cast<const double2*>(&nr->lo[0]);
+        nd.l2h0 = *reinterpret_cast<const double2*>(&nr->lo[2]);
+        nd.h12 = *reinterpret_cast<const double2*>(&nr->hi[1]);
+        const int2 topo = *reinterpret_cast<const int2*>(&nr->first);
+        const int32_t first = has ? topo.x : 0;
+        const uint32_t meta = has ? (uint32_t)topo.y : 0u;
+        const uint32_t kids = (has && !(meta & kLeafBit)) ? children_in_box(nd, meta & 0xffu, wlx, wly, wlz, whx, why, whz) : 0u;
         // a leaf contributes its points (contiguous in leaf order) to the candidate list
-        const int lc0 = (has0 && (meta0 & kLeafBit)) ? (int)(meta0 & ~kLeafBit) : 0;
-        const int lc1 = (has1 && (meta1 & kLeafBit)) ? (int)(meta1 & ~kLeafBit) : 0;
-        const int lcnt = lc0 + lc1;
+        const int lcnt = (has && (meta & kLeafBit)) ? (int)(meta & ~kLeafBit) : 0;
         int ltot;
         const int lincl = wave_incl_scan(lcnt, &ltot);
         const int lpos = nleaf + lincl - lcnt;
         if (lcnt > 0 && lpos + lcnt <= kWaveCandCap)
-          for (int c = 0; c < lcnt; c++) plist[lpos + c] = c < lc0 ? first0 + c : first1 + (c - lc0);
+          for (int c = 0; c < lcnt; c++) plist[lpos + c] = first + c;
         nleaf += ltot;
-        const int n0 = __builtin_popcount(kids0), nch = n0 + __builtin_popcount(kids1);
+        const int nch = __builtin_popcount(kids);
         int tot;
         const int incl = wave_incl_scan(nch, &tot);
         tail -= batch;  // the popped entries are in registers; children overwrite them
@@ -572,17 +566,11 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
           return;
         }
         int off = tail + incl - nch;
-        uint32_t kk = kids0;
+        uint32_t kk = kids;
         while (kk) {
           const uint32_t o = (uint32_t)__builtin_ctz(kk);
           kk &= kk - 1u;
-          queue[off++] = first0 + __builtin_popcount(meta0 & 0xffu & ((1u << o) - 1u));
-        }
-        kk = kids1;
-        while (kk) {
-          const uint32_t o = (uint32_t)__builtin_ctz(kk);
-          kk &= kk - 1u;
-          queue[off++] = first1 + __builtin_popcount(meta1 & 0xffu & ((1u << o) - 1u));
+          queue[off++] = first + __builtin_popcount(meta & 0xffu & ((1u << o) - 1u));
         }
         tail += tot;
         if (kDbg && a.dbg && lane == 0) atomicAdd(&a.dbg[5], 1ull);
