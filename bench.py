@@ -288,6 +288,8 @@ def main() -> int:
     ap.add_argument("--scene", action="store_true",
                     help="a LiDAR-like scene pair (icp_synth_scene: ground + walls scanned from two poses, "
                          "range-dependent density, 1 mm grid) instead of config 4's Gaussian blob")
+    ap.add_argument("--scene-outliers", type=float, default=None,
+                    help="--scene: the source's outlier fraction (default the generator's 0.002)")
     ap.add_argument("--config", action="append", default=[], metavar="KEY=VALUE",
                     help="icp_hip_config field for the context (A/B of search options), repeatable")
     ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "traffic_latest.json"),
@@ -319,7 +321,8 @@ def main() -> int:
 
     n = args.points
     t_setup = time.perf_counter()
-    tgt, src, T_true = icp.synth_scene(n) if args.scene else icp.synth_pair(n)
+    scene_kw = {} if args.scene_outliers is None else {"outlier_fraction": args.scene_outliers}
+    tgt, src, T_true = icp.synth_scene(n, **scene_kw) if args.scene else icp.synth_pair(n)
     if args.duplicates > 1:
         tgt = np.repeat(tgt[: n // args.duplicates + 1], args.duplicates, axis=0)[:n]
     if args.quantize > 0:

@@ -118,6 +118,7 @@ struct NNLaunch {
   int certify_prev;         // previous-match certificate mode (icp_hip_config.certify_prev)
   WaveStat* wstat;          // per-wave covariance records (null: none; the cull pass does it all)
   const IterDev* fz;        // the band of this iterate (IterDev::fz_*)
+  int32_t ball_queue_off;   // k_nn_ball: byte offset of its follow-up queue in LDS
 };
 
 // Threads per block of the per-thread search kernels for a given stack depth.

@@ -464,8 +464,10 @@ __device__ __forceinline__ uint32_t key16(double v) {
 // the second best and the position of the best.
 // Stack entry: bits 0..31 first child record, 32..39 remaining octants, 40..47 the parent's
 // child mask, 48..63 key16 lower bound of the remaining children's s.
-__device__ __forceinline__ void fast_dfs(const NNLaunch& a, double qx, double qy, double qz, unsigned long long* st,
-                                         int bs, double& best, double& second, int32_t& bpos) {
+// budget > 0: give up after that many node visits (returns false: the results are incomplete).
+__device__ __forceinline__ bool fast_dfs(const NNLaunch& a, double qx, double qy, double qz, unsigned long long* st,
+                                         int bs, double& best, double& second, int32_t& bpos, int budget = 0) {
+  int visits = 0;
   double thr = __builtin_inf();
   uint32_t thr_key = key16(__builtin_inf());
   int sp = 0;
@@ -475,6 +477,7 @@ __device__ __forceinline__ void fast_dfs(const NNLaunch& a, double qx, double qy
   double s = box_s(lx, ly, lz, hx, hy, hz, qx, qy, qz);
   while (true) {
     bool entered = false;
+    if (budget > 0 && ++visits > budget) return false;
     if (!(s > thr)) {
       const int2 topo = *reinterpret_cast<const int2*>(&a.nodes[node].first);
       const int32_t first = topo.x;
@@ -566,6 +569,7 @@ __device__ __forceinline__ void fast_dfs(const NNLaunch& a, double qx, double qy
     }
     if (!found) break;
   }
+  return true;
 }
 
 // Append the lanes with `want` to a list, one atomic per wave, lane order kept (the lists stay

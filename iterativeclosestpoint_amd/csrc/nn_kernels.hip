@@ -1236,18 +1236,123 @@ __device__ __forceinline__ void exact_query(const NNLaunch& a, int64_t i, unsign
 }
 
 // The per-lane certified search for query i; a query it cannot certify gets the reference-order
-// DFS right away.
-__device__ __forceinline__ void lane_query(const NNLaunch& a, int64_t i, unsigned long long* st, int bs) {
+// DFS right away. budget > 0: a search that needs more node visits gives up (returns false, nothing
+// written: the wave-cooperative search takes it).
+// *found: the best fl(d2) it had found when it gave up (a point's: an upper bound for the next search).
+__device__ __forceinline__ bool lane_query(const NNLaunch& a, int64_t i, unsigned long long* st, int bs,
+                                           int budget = 0, double* found = nullptr) {
   const double qx = a.x[i], qy = a.y[i], qz = a.z[i];
   double best = __builtin_inf(), second = __builtin_inf();
   int32_t bpos = -1;
-  fast_dfs(a, qx, qy, qz, st, bs, best, second, bpos);
+  if (!fast_dfs(a, qx, qy, qz, st, bs, best, second, bpos, budget)) {
+    if (found) *found = best;
+    return false;
+  }
   if (certified(best, second, a.init_best)) {
     a.pos_out[i] = bpos;
     a.dist_out[i] = __builtin_sqrt(best);
   } else {
     exact_query(a, i, st, bs);
   }
+  return true;
+}
+
+// Node visits a per-lane follow-up search may take before the wave-cooperative search takes over.
+// A query far (relative to the local point spacing) from a dense surface needs every leaf whose
+// box comes within its nearest distance: on the scene workload's outliers (metres above a ground
+// sampled every few mm) up to ~30k visits of one lane, ~1 us of dependent loads each (the
+// reference's DFS needs as many: tools/scene_probe.py). 156 on average there.
+constexpr int kLaneBudget = 768;
+constexpr int kBBStack = 2048;  // the cooperative search's node stack (int32 in LDS)
+
+// The wave-cooperative certified search of one query (every lane of the wave): branch and bound
+// over the octree, up to 64 nodes per step (one per lane, LIFO), each node re-tested against the
+// prune bound thr = best (1 + 2^-47) of the wave's best so far (exact as fast_dfs: a node is
+// skipped only when its squared box distance s exceeds thr, so every point of the certificate
+// window is scanned), leaves scanned by their lane, the best reduced over the wave every step.
+// u: an upper bound of the query's nearest fl(d2) (inf: none). Returns false when the stack
+// overflows (nothing written; the caller runs the reference-order DFS); otherwise writes the
+// certified result, or runs the reference-order DFS on lane 0 for a tie.
+__device__ __noinline__ bool wave_bb(const NNLaunch& a, int64_t i, double u, int32_t* stack,
+                                     unsigned long long* dfs_st, int lane) {
+  const double qx = a.x[i], qy = a.y[i], qz = a.z[i];
+  double best = __builtin_inf(), second = __builtin_inf();
+  int32_t bpos = 0x7fffffff;
+  double thr = (u <= 0x1p900) ? u * (1.0 + kFastPrune) : __builtin_inf();
+  if (lane == 0) stack[0] = 0;
+  int tail = 1;
+  bool over = false;
+  wave_lds_fence();
+  while (tail > 0) {
+    const int batch = tail < 64 ? tail : 64;
+    const bool has = lane < batch;
+    const int32_t nid = has ? stack[tail - batch + lane] : 0;
+    tail -= batch;
+    const NodeRec* rr = a.nodes + nid;
+    const double2 l01 = *reinterpret_cast<const double2*>(&rr->lo[0]);
+    const double2 l2h0 = *reinterpret_cast<const double2*>(&rr->lo[2]);
+    const double2 h12 = *reinterpret_cast<const double2*>(&rr->hi[1]);
+    const int2 topo = *reinterpret_cast<const int2*>(&rr->first);
+    const uint32_t meta = (uint32_t)topo.y;
+    // pushed against an older (larger) bound: test the node itself again
+    const bool live = has && !(box_s(l01.x, l01.y, l2h0.x, l2h0.y, h12.x, h12.y, qx, qy, qz) > thr);
+    uint32_t kids = 0;
+    if (live && (meta & kLeafBit)) {
+      const int32_t cnt = (int32_t)(meta & ~kLeafBit);
+      for (int32_t k = 0; k < cnt; k++) {
+        const TgtPt* p = a.pts + topo.x + k;
+        const double2 pxy = *reinterpret_cast<const double2*>(&p->x);
+        const double dx = pxy.x - qx, dy = pxy.y - qy, dz = p->z - qz;
+        const double d2 = dx * dx + dy * dy + dz * dz;
+        if (d2 < best) {
+          second = best;
+          best = d2;
+          bpos = topo.x + k;
+        } else if (d2 < second) {
+          second = d2;
+        }
+      }
+    } else if (live) {
+      kids = children_in_ball(rr, meta & 0xffu, qx, qy, qz, thr);
+    }
+    const int nch = __builtin_popcount(kids);
+    int tot;
+    const int incl = wave_incl_scan(nch, &tot);
+    if (tail + tot > kBBStack) {
+      over = true;
+      break;
+    }
+    wave_lds_fence();  // this step's pops are read before the pushes overwrite them
+    int off = tail + incl - nch;
+    uint32_t kk = kids;
+    while (kk) {
+      const uint32_t o = (uint32_t)__builtin_ctz(kk);
+      kk &= kk - 1u;
+      stack[off++] = topo.x + __builtin_popcount((meta & 0xffu) & ((1u << o) - 1u));
+    }
+    tail += tot;
+    const double gb = wave_min_d(best);
+    const double t2 = gb * (1.0 + kFastPrune);
+    thr = t2 < thr ? t2 : thr;
+    wave_lds_fence();
+  }
+  wave_lds_fence();
+  if (over) return false;
+  // the wave's best, and its second: the smallest of the other lanes' bests and the best lane's
+  // second (a best held by two lanes is its own second: a tie)
+  const double gb = wave_min_d(best);
+  const unsigned long long at = __ballot(best == gb);
+  const double gs = __popcll(at) > 1 ? gb : wave_min_d(best == gb ? second : best);
+  const int32_t gp = (int32_t)__builtin_amdgcn_readlane(bpos, __builtin_ctzll(at ? at : 1ull));
+  if (certified(gb, gs, a.init_best)) {
+    if (lane == 0) {
+      a.pos_out[i] = gp;
+      a.dist_out[i] = __builtin_sqrt(gb);
+    }
+  } else if (lane == 0) {
+    exact_query(a, i, dfs_st, 1);
+  }
+  return true;
 }
 
 __global__ void __launch_bounds__(64) k_nn_ball(NNLaunch a) {
@@ -1264,8 +1369,45 @@ __global__ void __launch_bounds__(64) k_nn_ball(NNLaunch a) {
       exact_query(a, a.fb_list[j], lds_raw + lane, 64);
     wave_lds_fence();
   }
-  // a group's own DFS stack (its first lane's): the group's candidate area, after its scan
-  unsigned long long* gstack = reinterpret_cast<unsigned long long*>(plist);
+  // The follow-ups of the ball queries (a per-lane certified search, or the reference-order DFS)
+  // are queued per wave and run 64 at a time, one query per lane with its own DFS stack column
+  // (the exact list's layout), once the queue is nearly full and at the end. (One lane of the
+  // query's group ran each inline before: 1 lane in 16 busy. On a dense 2.5-D scan early in a
+  // registration the queries sit ~0.3 m off surfaces sampled every few mm, every ball overflows,
+  // and that serial tail took 21 ms per iterate at 1M points.)
+  int32_t* fq = reinterpret_cast<int32_t*>(reinterpret_cast<unsigned char*>(lds_raw) + a.ball_queue_off);
+  double* fqu = reinterpret_cast<double*>(fq + 64);  // each entry's guess u (an upper bound, or inf)
+  int qn = 0;  // wave-uniform
+  // A per-lane search that exceeds kLaneBudget node visits is handed to the wave-cooperative
+  // search (the whole wave on one query), one after the other once the lanes are done.
+  auto flush = [&]() {
+    wave_lds_fence();
+    bool handed = false;
+    int32_t e = 0;
+    double qu = __builtin_inf();
+    if (lane < qn) {
+      e = fq[lane];
+      qu = fqu[lane];
+      const int64_t iq = e & 0x3fffffff;
+      // an abandoned search's best so far (a point's fl(d2)) bounds the cooperative search
+      double found = __builtin_inf();
+      if ((e >> 30) == 1) handed = !lane_query(a, iq, lds_raw + lane, 64, kLaneBudget, &found);
+      else exact_query(a, iq, lds_raw + lane, 64);
+      qu = found < qu ? found : qu;
+    }
+    wave_lds_fence();
+    for (unsigned long long hm = __ballot(handed); hm; hm &= hm - 1) {
+      const int k = __builtin_ctzll(hm);
+      const int64_t iq = __builtin_amdgcn_readlane(e, k) & 0x3fffffff;
+      const double uq = readlane_d(qu, k);
+      // the stack in the DFS columns' area (free now); the fallback DFS after it, in the same area
+      if (!wave_bb(a, iq, uq, reinterpret_cast<int32_t*>(lds_raw), lds_raw, lane) && lane == 0)
+        exact_query(a, iq, lds_raw, 1);
+      wave_lds_fence();
+    }
+    qn = 0;
+    wave_lds_fence();
+  };
   const unsigned cnt = a.fb_count[1];
   for (unsigned j0 = blockIdx.x * kBallGroups; j0 < cnt; j0 += gridDim.x * kBallGroups) {
     const unsigned j = j0 + g;
@@ -1394,14 +1536,21 @@ __global__ void __launch_bounds__(64) k_nn_ball(NNLaunch a) {
         follow = 2;
       }
     }
-    wave_lds_fence();  // the group's candidate area is free: its first lane's DFS stack
-    if (follow != 0 && gl == 0) {
+    // queue the follow-ups (one entry per group: its leader lane)
+    const bool fol = follow != 0 && gl == 0;
+    const unsigned long long fm = __ballot(fol);
+    if (fol) {
       atomicAdd(a.fb_count + (follow == 1 ? 2 : 3), 1u);  // counted for the iteration record
-      if (follow == 1) lane_query(a, i, gstack, 1);
-      else exact_query(a, i, gstack, 1);
+      fq[qn + mask_rank(fm)] = (int32_t)i | (follow << 30);
+      // an overflowing ball's guess bounds the nearest distance (a guess the ball did not cover
+      // does not, nor does an unusable one)
+      fqu[qn + mask_rank(fm)] = (overflow && u <= 0x1p900) ? u : __builtin_inf();
     }
+    qn += __popcll(fm);
+    if (qn > 64 - kBallGroups) flush();
     wave_lds_fence();
   }
+  if (qn > 0) flush();
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1623,10 +1772,12 @@ hipError_t launch_nn(const NNLaunch& a, hipStream_t s) {
   const int64_t bq = (a.n + kBallGroups - 1) / kBallGroups;
   size_t bshm = (size_t)levels * 64 * sizeof(unsigned long long);
   if (bshm < (size_t)kBallLdsBytes) bshm = kBallLdsBytes;
-  static_assert(kBallGPoints * 4 >= 64 * 8, "a group's DFS stack (stride 1) holds >= 64 levels");
-  if (levels > kBallGPoints * 4 / 8) return hipErrorInvalidValue;
+  NNLaunch b = a;
+  if (bshm < (size_t)kBBStack * sizeof(int32_t)) bshm = (size_t)kBBStack * sizeof(int32_t);  // wave_bb's stack
+  b.ball_queue_off = (int32_t)bshm;  // the follow-up queue (64 entries + guesses) after the stacks and lists
+  bshm += 64 * (sizeof(int32_t) + sizeof(double));
   hipExtLaunchKernelGGL(k_nn_ball, dim3((unsigned)(bq < 8192 ? bq : 8192)), dim3(64), (uint32_t)bshm, s, nullptr,
-                        nullptr, 0u, a);
+                        nullptr, 0u, b);
   return hipGetLastError();
 }
 

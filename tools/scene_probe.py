@@ -1,0 +1,45 @@
+#!/usr/bin/env python3
+"""Per-iterate search-path counts and kernel times on the LiDAR-like scene (icp_synth_scene),
+with scene overrides from the command line (KEY=VALUE), to find what makes a follow-up path slow.
+
+usage: python3 tools/scene_probe.py N ITERS [KEY=VALUE ...]
+"""
+import json
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+import iterativeclosestpoint_amd as icp  # noqa: E402
+
+n = int(sys.argv[1])
+iters = int(sys.argv[2])
+kw = {}
+cfg = {}
+for a in sys.argv[3:]:
+    k, v = a.split("=", 1)
+    if k.startswith("cfg."):
+        cfg[k[4:]] = float(v) if "." in v else int(v)
+    else:
+        kw[k] = float(v) if "." in v or "e" in v else int(v)
+tgt, src, _ = icp.synth_scene(n, **kw)
+with icp.Context(0, icp.config(debug_counters=1, timing_stride=1, **cfg)) as ctx:
+    ctx.set_target(tgt, 10, 20, icp.RULES_ENGINE)
+    ctx.set_source(src)
+    T = None
+    for it in range(iters):
+        t0 = time.perf_counter()
+        st = ctx.iterate(T, it, icp.RULES_ENGINE, 3.0)
+        wall = (time.perf_counter() - t0) * 1e3
+        c = ctx.debug_counters()
+        nn_ms, it_ms = ctx.last_timing()
+        out = {"it": it, "wall_ms": round(wall, 3), "search_ms": round(nn_ms, 4), "iter_ms": round(it_ms, 4),
+               "ball": st.n_ball_search, "lane": st.n_lane_search, "exact": st.n_fallback, "valid": st.valid,
+               "rmse": st.rmse}
+        for k in ("waves", "overflow_waves", "not_joined", "not_covered", "ball_overflow", "ball_points",
+                  "fp64_scan_waves", "cache_hits", "scan_pairs", "staged_points"):
+            out[k] = c.get(k)
+        print(json.dumps(out), flush=True)
+        T = icp.best_fit_from_stats(st)
