@@ -465,11 +465,13 @@ __device__ __forceinline__ uint32_t key16(double v) {
 // Stack entry: bits 0..31 first child record, 32..39 remaining octants, 40..47 the parent's
 // child mask, 48..63 key16 lower bound of the remaining children's s.
 // budget > 0: give up after that many node visits (returns false: the results are incomplete).
+// thr0: the initial prune bound, u (1 + 2^-47) for an upper bound u of the nearest fl(d2) (inf: none).
 __device__ __forceinline__ bool fast_dfs(const NNLaunch& a, double qx, double qy, double qz, unsigned long long* st,
-                                         int bs, double& best, double& second, int32_t& bpos, int budget = 0) {
+                                         int bs, double& best, double& second, int32_t& bpos, int budget = 0,
+                                         double thr0 = __builtin_inf()) {
   int visits = 0;
-  double thr = __builtin_inf();
-  uint32_t thr_key = key16(__builtin_inf());
+  double thr = thr0;
+  uint32_t thr_key = key16(thr0);
   int sp = 0;
   int32_t node = 0;
   const NodeRec* r0 = a.nodes;

@@ -1239,12 +1239,14 @@ __device__ __forceinline__ void exact_query(const NNLaunch& a, int64_t i, unsign
 // DFS right away. budget > 0: a search that needs more node visits gives up (returns false, nothing
 // written: the wave-cooperative search takes it).
 // *found: the best fl(d2) it had found when it gave up (a point's: an upper bound for the next search).
+// u: an upper bound of the nearest fl(d2) (inf: none), the search's initial prune bound.
 __device__ __forceinline__ bool lane_query(const NNLaunch& a, int64_t i, unsigned long long* st, int bs,
-                                           int budget = 0, double* found = nullptr) {
+                                           int budget = 0, double* found = nullptr, double u = __builtin_inf()) {
   const double qx = a.x[i], qy = a.y[i], qz = a.z[i];
   double best = __builtin_inf(), second = __builtin_inf();
   int32_t bpos = -1;
-  if (!fast_dfs(a, qx, qy, qz, st, bs, best, second, bpos, budget)) {
+  const double thr0 = u <= 0x1p900 ? u * (1.0 + kFastPrune) : __builtin_inf();
+  if (!fast_dfs(a, qx, qy, qz, st, bs, best, second, bpos, budget, thr0)) {
     if (found) *found = best;
     return false;
   }
@@ -1273,7 +1275,7 @@ constexpr int kBBStack = 2048;  // the cooperative search's node stack (int32 in
 // u: an upper bound of the query's nearest fl(d2) (inf: none). Returns false when the stack
 // overflows (nothing written; the caller runs the reference-order DFS); otherwise writes the
 // certified result, or runs the reference-order DFS on lane 0 for a tie.
-__device__ __noinline__ bool wave_bb(const NNLaunch& a, int64_t i, double u, int32_t* stack,
+__device__ __forceinline__ bool wave_bb(const NNLaunch& a, int64_t i, double u, int32_t* stack,
                                      unsigned long long* dfs_st, int lane) {
   const double qx = a.x[i], qy = a.y[i], qz = a.z[i];
   double best = __builtin_inf(), second = __builtin_inf();
@@ -1391,7 +1393,7 @@ __global__ void __launch_bounds__(64) k_nn_ball(NNLaunch a) {
       const int64_t iq = e & 0x3fffffff;
       // an abandoned search's best so far (a point's fl(d2)) bounds the cooperative search
       double found = __builtin_inf();
-      if ((e >> 30) == 1) handed = !lane_query(a, iq, lds_raw + lane, 64, kLaneBudget, &found);
+      if ((e >> 30) == 1) handed = !lane_query(a, iq, lds_raw + lane, 64, kLaneBudget, &found, qu);
       else exact_query(a, iq, lds_raw + lane, 64);
       qu = found < qu ? found : qu;
     }
