@@ -138,7 +138,13 @@ typedef struct icp_hip_config {
                               it, an RCCL communicator's asynchronous error (a peer process that
                               died, a broken link: ncclCommGetAsyncError) is checked while the
                               host waits, with the same outcome                           dflt 0 */
-  int32_t reserved[6];     /* zero (fields of later versions of this header)                    */
+  int32_t no_warmup;       /* 0: the first context a process creates on a device with a given set of
+                              search options runs a 3-iterate registration of a 4096-point
+                              synthetic pair on a private context first (~5 ms, once): HIP
+                              loads a kernel's code and sizes its scratch at the kernel's first
+                              launch, which otherwise lands in the first real iterate (+1.3 ms
+                              at 10M); 1: no warm-up                                     dflt 0 */
+  int32_t reserved[5];     /* zero (fields of later versions of this header)                    */
   uint32_t config_version; /* ICP_HIP_CONFIG_VERSION, set by icp_hip_config_default; create_ex
                               rejects any other value (a struct from another header version)     */
 } icp_hip_config;

@@ -220,7 +220,10 @@ __device__ __forceinline__ T block_tree_last_sc1(const T* in, int64_t n, T* sm) 
 // 100k queries (25 moment parts, 98 cull blocks) -2 us per iteration; at 1221 cull blocks (a
 // 1.25M shard) +15 us, at 2442 moment parts (10M) +5 us.
 // the moments blocks: fused up to 512 parts (2M queries)
-constexpr int kFuseMaxMomentParts = 512;
+#ifndef ICP_FUSE_MOMENT_PARTS
+#define ICP_FUSE_MOMENT_PARTS 512
+#endif
+constexpr int kFuseMaxMomentParts = ICP_FUSE_MOMENT_PARTS;
 // the cull blocks (256 search waves each: 611 at 10M) up to 1024 blocks (16.7M queries)
 constexpr int kFuseMaxCullBlocks = 1024;
 constexpr int kTicketLine = 32;                      // uints per counter line (128 B)
@@ -251,7 +254,10 @@ __device__ __forceinline__ bool publish_part_last(T* part, const T& mine, unsign
 // Residual moments of the rank's queries in fixed parts of kMomPart queries, once every search
 // kernel has written its residuals: deterministic whatever order the queries were settled in.
 // Thread t of block p holds queries p kMomPart + t + 256 e (e < kMomPer, coalesced).
-constexpr int kMomPer = 16;
+#ifndef ICP_MOM_PER
+#define ICP_MOM_PER 16
+#endif
+constexpr int kMomPer = ICP_MOM_PER;
 constexpr int kMomPart = 256 * kMomPer;
 
 // mean = sum/row; std = sqrt(variance/row) (icpengine.cpp:235-245); threshold rule of the caller

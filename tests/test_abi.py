@@ -56,3 +56,20 @@ def test_create_multi_rejects_bad_arguments_without_a_gpu(icp):
     assert L.icp_hip_create_multi(C.byref(h), 2, two, None, 7) == -1              # unknown transport
     assert L.icp_hip_create_multi(C.byref(h), 0, two, None, icp.XPORT_AUTO) == -1  # empty list
     assert not h.value
+
+
+def test_create_ex_validates_config_without_a_gpu(icp):
+    """icp_hip_create_ex checks the config (version, ranges, the no_warmup switch) before any
+    device call: a struct of another header version or an out-of-range field is EINVAL."""
+    import ctypes as C
+    L = icp.lib()
+    h = C.c_void_p()
+    cfg = icp.config()
+    assert cfg.no_warmup == 0 and cfg.config_version == 2
+    for field, bad in (("no_warmup", 2), ("peer_timeout_ms", -1), ("scan_groups", 3), ("config_version", 1)):
+        c = icp.config()
+        setattr(c, field, bad)
+        assert L.icp_hip_create_ex(C.byref(h), 0, C.byref(c)) == icp.EINVAL, field
+        assert not h.value
+        msg = L.icp_hip_last_error().decode()
+        assert (field if field != "config_version" else "config_version") in msg, msg
