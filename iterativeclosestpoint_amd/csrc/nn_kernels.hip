@@ -227,6 +227,9 @@ static_assert(kStatLds <= kWaveLds, "the record's reduction fits the wave's LDS 
 // moved, no candidate cache; lanes 32..63 idle).
 // DBG: the instance of a context with debug counters (ICP_DBG_* slots); the product instances
 // carry none of their code.
+#ifndef ICP_GUESS_LANES
+#define ICP_GUESS_LANES 64  // lanes sharing their first-iterate guess points (16, 32, 64)
+#endif
 template <bool APPLY, int NG, bool CERT, bool HALF, bool DBG>
 __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, const int lane, unsigned char* wl) {
   constexpr bool kDbg = DBG && kDbgCounts;
@@ -262,6 +265,7 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
   PCLK(t_p0);
   // Phase 1: the guess (any value is safe: certification also requires best <= u).
   double u = __builtin_inf();
+  int32_t gpos = -1;  // (first iterate) the target point whose distance is u
   bool safe = false;  // the previous match certified from its separation: no search
   if (active && finite_q && a.have_prev) {
     // the previous match is a candidate: its fl(d2) from the moved query bounds the nearest
@@ -284,7 +288,9 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
         const TgtPt* p = a.pts + topo.x + k;
         const double dx = p->x - qx, dy = p->y - qy, dz = p->z - qz;
         const double d2 = dx * dx + dy * dy + dz * dz;
-        u = d2 < u ? d2 : u;
+        const bool t = d2 < u;
+        u = t ? d2 : u;
+        if (!APPLY) gpos = t ? topo.x + k : gpos;
       }
     };
     while (true) {
@@ -340,6 +346,44 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
       if (o1 & 1u) lx = mx; else hx = mx;
       if (o1 & 2u) ly = my; else hy = my;
       if (o1 & 4u) lz = mz; else hz = mz;
+    }
+  }
+
+  // Phase 1a (first iterate): the 64 lanes hold one kd bucket of queries, near each other: every
+  // lane also tries the other lanes' guess points (fp32 offsets from a wave-uniform query; the
+  // nearest one's exact fl(d2) becomes u when smaller). A lane whose own leaf guessed poorly (a
+  // query near its leaf's boundary) gets its neighbours' points: smaller boxes, fewer overflows
+  // and follow-up searches in the iterate with the loosest guesses. Measured at 10M (one MI355X,
+  // profiles/r21/ab_first_iterate_guess.txt): lanes not joining their wave's box 14651 -> 1214,
+  // overflowing waves 3546 -> 1075, first iterate 2.78 -> 2.52 ms (16 lanes: 2.61, 32: 2.58).
+  if (!APPLY && !a.have_prev) {
+    constexpr int kGL = ICP_GUESS_LANES;
+    const double rx = __shfl(qx, lane & (64 - kGL), kWave), ry = __shfl(qy, lane & (64 - kGL), kWave),
+                 rz = __shfl(qz, lane & (64 - kGL), kWave);
+    float gx = 3.0e38f, gy = 3.0e38f, gz = 3.0e38f;
+    if (gpos >= 0) {
+      const TgtPt* p = a.pts + gpos;
+      gx = (float)(p->x - rx);
+      gy = (float)(p->y - ry);
+      gz = (float)(p->z - rz);
+    }
+    const float fx = (float)(qx - rx), fy = (float)(qy - ry), fz = (float)(qz - rz);
+    float bd = 3.0e38f;
+    int bm = 0;
+#pragma unroll
+    for (int m = 1; m < kGL; m++) {
+      const float ox = __shfl_xor(gx, m, kWave) - fx, oy = __shfl_xor(gy, m, kWave) - fy,
+                  oz = __shfl_xor(gz, m, kWave) - fz;
+      const float d = __builtin_fmaf(oz, oz, __builtin_fmaf(oy, oy, ox * ox));
+      bm = d < bd ? m : bm;
+      bd = d < bd ? d : bd;
+    }
+    const int32_t op = __shfl(gpos, lane ^ bm, kWave);
+    if (active && finite_q && bm != 0 && op >= 0) {
+      const TgtPt* p = a.pts + op;
+      const double dx = p->x - qx, dy = p->y - qy, dz = p->z - qz;
+      const double d2 = dx * dx + dy * dy + dz * dz;
+      u = d2 < u ? d2 : u;
     }
   }
 
