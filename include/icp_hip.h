@@ -186,9 +186,9 @@ typedef struct icp_hip_config {
                                     their box left B+                                        */
 #define ICP_DBG_WALK_LOOSE 25   /* waves whose box lay inside B+ but walked because B+ was loose */
 #define ICP_DBG_GROUP_POINTS 26 /* fp32 scan: points staged, summed over the scan groups       */
-#define ICP_DBG_EXIT_FWD 27     /* walk_moved waves whose box left B+ on the side it moves to  */
-#define ICP_DBG_EXIT_BACK 28    /* ... on the side opposite to its motion                       */
-#define ICP_DBG_EXIT_GREW 29    /* ... and whose box is wider than B+ on some axis              */
+#define ICP_DBG_BB_QUERIES 27   /* ball-search follow-ups taken by the wave-cooperative search  */
+#define ICP_DBG_BB_STEPS 28     /* their steps (up to 64 nodes each)                            */
+#define ICP_DBG_LANE_HANDED 29  /* per-lane follow-ups that ran out of their node budget        */
 #define ICP_DBG_FZ_RECOMPUTE 30 /* waves whose covariance record the cull recomputes (queries
                                    left to the other searches)                                 */
 #define ICP_DBG_FZ_BAND 31      /* queries in the band around the previous threshold           */

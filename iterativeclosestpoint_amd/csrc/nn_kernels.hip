@@ -1307,8 +1307,14 @@ __device__ __forceinline__ bool lane_query(const NNLaunch& a, int64_t i, unsigne
 // A query far (relative to the local point spacing) from a dense surface needs every leaf whose
 // box comes within its nearest distance: on the scene workload's outliers (metres above a ground
 // sampled every few mm) up to ~30k visits of one lane, ~1 us of dependent loads each (the
-// reference's DFS needs as many: tools/scene_probe.py). 156 on average there.
-constexpr int kLaneBudget = 768;
+// reference's DFS needs as many: tools/scene_probe.py). A wave's queue runs its lanes' searches
+// together, so the longest one sets its time: the budget bounds that, and the cooperative search
+// (64 nodes a step) takes the rest. Measured (profiles/r21/ab_lane_budget.txt, scene 20/5): 768
+// -> 64 visits: 1M 320 -> 635 Mcorr/s, 10M 600 -> 677; config 4 and config 3 unchanged.
+#ifndef ICP_LANE_BUDGET
+#define ICP_LANE_BUDGET 64
+#endif
+constexpr int kLaneBudget = ICP_LANE_BUDGET;
 constexpr int kBBStack = 2048;  // the cooperative search's node stack (int32 in LDS)
 
 // The wave-cooperative certified search of one query (every lane of the wave): branch and bound
@@ -1326,7 +1332,7 @@ __device__ __forceinline__ bool wave_bb(const NNLaunch& a, int64_t i, double u, 
   int32_t bpos = 0x7fffffff;
   double thr = (u <= 0x1p900) ? u * (1.0 + kFastPrune) : __builtin_inf();
   if (lane == 0) stack[0] = 0;
-  int tail = 1;
+  int tail = 1, steps = 0;
   bool over = false;
   wave_lds_fence();
   while (tail > 0) {
@@ -1380,9 +1386,14 @@ __device__ __forceinline__ bool wave_bb(const NNLaunch& a, int64_t i, double u, 
     const double gb = wave_min_d(best);
     const double t2 = gb * (1.0 + kFastPrune);
     thr = t2 < thr ? t2 : thr;
+    ++steps;
     wave_lds_fence();
   }
   wave_lds_fence();
+  if (a.dbg && lane == 0) {
+    atomicAdd(&a.dbg[27], 1ull);
+    atomicAdd(&a.dbg[28], (unsigned long long)steps);
+  }
   if (over) return false;
   // the wave's best, and its second: the smallest of the other lanes' bests and the best lane's
   // second (a best held by two lanes is its own second: a tie)
@@ -1442,6 +1453,7 @@ __global__ void __launch_bounds__(64) k_nn_ball(NNLaunch a) {
       qu = found < qu ? found : qu;
     }
     wave_lds_fence();
+    if (a.dbg && lane == 0) atomicAdd(&a.dbg[29], (unsigned long long)__popcll(__ballot(handed)));
     for (unsigned long long hm = __ballot(handed); hm; hm &= hm - 1) {
       const int k = __builtin_ctzll(hm);
       const int64_t iq = __builtin_amdgcn_readlane(e, k) & 0x3fffffff;

@@ -39,7 +39,8 @@ with icp.Context(0, icp.config(debug_counters=1, timing_stride=1, **cfg)) as ctx
                "ball": st.n_ball_search, "lane": st.n_lane_search, "exact": st.n_fallback, "valid": st.valid,
                "rmse": st.rmse}
         for k in ("waves", "overflow_waves", "not_joined", "not_covered", "ball_overflow", "ball_points",
-                  "fp64_scan_waves", "cache_hits", "scan_pairs", "staged_points"):
+                  "fp64_scan_waves", "cache_hits", "scan_pairs", "staged_points", "bb_queries", "bb_steps",
+                  "lane_handed"):
             out[k] = c.get(k)
         print(json.dumps(out), flush=True)
         T = icp.best_fit_from_stats(st)
