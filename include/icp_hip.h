@@ -182,6 +182,8 @@ typedef struct icp_hip_config {
 #define ICP_DBG_START_NODES 21   /* start nodes taken from the cell tables / descent levels    */
 #define ICP_DBG_WINNER_PREV 22   /* winner-count build: joined lanes whose winner is the previous match */
 #define ICP_DBG_WINNER_LANES 23  /* winner-count build: joined lanes with an fp32 winner          */
+#define ICP_DBG_BB_OVERFLOW 23   /* other builds: cooperative searches whose frontier still
+                                    overflowed after their restarts (the reference-order DFS ran) */
 #define ICP_DBG_WALK_MOVED 24   /* waves with a record of this generation that walked because
                                     their box left B+                                        */
 #define ICP_DBG_WALK_LOOSE 25   /* waves whose box lay inside B+ but walked because B+ was loose */

@@ -31,7 +31,7 @@ DBG_NAMES = {0: "waves", 1: "overflow_waves", 2: "not_joined", 3: "not_covered",
              8: "fp64_scan_waves", 9: "staged_points", 10: "scan_pairs", 11: "scan_rounds",
              12: "cache_hits", 13: "cache_stores",
              5: "walk_batches", 6: "no_guess", 7: "candidates", 14: "ball_overflow", 15: "ball_points",
-             21: "start_nodes", 20: "winner_prev_waves", 22: "winner_prev", 23: "winner_lanes",
+             21: "start_nodes", 20: "winner_prev_waves", 22: "winner_prev", 23: "bb_overflow",
              18: "prev_cert_waves", 19: "prev_cert_lanes", 16: "halves", 17: "reused_entries",
              24: "walk_moved", 25: "walk_loose", 26: "group_points", 27: "bb_queries", 28: "bb_steps",
              29: "lane_handed", 30: "fz_recompute", 31: "fz_band"}

@@ -1322,77 +1322,102 @@ constexpr int kBBStack = 2048;  // the cooperative search's node stack (int32 in
 // prune bound thr = best (1 + 2^-47) of the wave's best so far (exact as fast_dfs: a node is
 // skipped only when its squared box distance s exceeds thr, so every point of the certificate
 // window is scanned), leaves scanned by their lane, the best reduced over the wave every step.
-// u: an upper bound of the query's nearest fl(d2) (inf: none). Returns false when the stack
-// overflows (nothing written; the caller runs the reference-order DFS); otherwise writes the
-// certified result, or runs the reference-order DFS on lane 0 for a tie.
+// u: an upper bound of the query's nearest fl(d2) (inf: none). A frontier that outgrows the stack
+// (a far query under a loose bound: every node within the bound is live) is searched again from
+// the root with the best point found so far as the bound, which prunes the frontier to the nodes
+// within the nearest distance (up to kBBPasses times while the bound shrinks). Returns false when
+// it still overflows (nothing written; the caller runs the reference-order DFS); otherwise writes
+// the certified result, or runs the reference-order DFS on lane 0 for a tie.
+constexpr int kBBPasses = 4;
 __device__ __forceinline__ bool wave_bb(const NNLaunch& a, int64_t i, double u, int32_t* stack,
                                      unsigned long long* dfs_st, int lane) {
   const double qx = a.x[i], qy = a.y[i], qz = a.z[i];
   double best = __builtin_inf(), second = __builtin_inf();
   int32_t bpos = 0x7fffffff;
   double thr = (u <= 0x1p900) ? u * (1.0 + kFastPrune) : __builtin_inf();
-  if (lane == 0) stack[0] = 0;
-  int tail = 1, steps = 0;
+  int steps = 0, passes = 0;
   bool over = false;
-  wave_lds_fence();
-  while (tail > 0) {
-    const int batch = tail < 64 ? tail : 64;
-    const bool has = lane < batch;
-    const int32_t nid = has ? stack[tail - batch + lane] : 0;
-    tail -= batch;
-    const NodeRec* rr = a.nodes + nid;
-    const double2 l01 = *reinterpret_cast<const double2*>(&rr->lo[0]);
-    const double2 l2h0 = *reinterpret_cast<const double2*>(&rr->lo[2]);
-    const double2 h12 = *reinterpret_cast<const double2*>(&rr->hi[1]);
-    const int2 topo = *reinterpret_cast<const int2*>(&rr->first);
-    const uint32_t meta = (uint32_t)topo.y;
-    // pushed against an older (larger) bound: test the node itself again
-    const bool live = has && !(box_s(l01.x, l01.y, l2h0.x, l2h0.y, h12.x, h12.y, qx, qy, qz) > thr);
-    uint32_t kids = 0;
-    if (live && (meta & kLeafBit)) {
-      const int32_t cnt = (int32_t)(meta & ~kLeafBit);
-      for (int32_t k = 0; k < cnt; k++) {
-        const TgtPt* p = a.pts + topo.x + k;
-        const double2 pxy = *reinterpret_cast<const double2*>(&p->x);
-        const double dx = pxy.x - qx, dy = pxy.y - qy, dz = p->z - qz;
-        const double d2 = dx * dx + dy * dy + dz * dz;
-        if (d2 < best) {
-          second = best;
-          best = d2;
-          bpos = topo.x + k;
-        } else if (d2 < second) {
-          second = d2;
-        }
-      }
-    } else if (live) {
-      kids = children_in_ball(rr, meta & 0xffu, qx, qy, qz, thr);
+  while (true) {
+    // a pass: every point it scans is counted once (best, second from this pass only)
+    best = __builtin_inf();
+    second = __builtin_inf();
+    bpos = 0x7fffffff;
+    const double thr0 = thr;
+    // the start nodes: the cell-table nodes of the box q +- sqrt(thr) (every point within the
+    // bound lies in it: the ball search's radius), else the root; the descent's levels skipped
+    int tail = 1;
+    if (a.cells && thr <= 0x1p900) {
+      const double amax = __builtin_fmax(__builtin_fabs(qx), __builtin_fmax(__builtin_fabs(qy), __builtin_fabs(qz)));
+      const double r = __builtin_sqrt(thr) * (1.0 + 0x1p-40) + amax * 0x1p-45;
+      tail = cell_starts<64, 2>(a, qx - r, qy - r, qz - r, qx + r, qy + r, qz + r, lane, 0, stack);
+    } else if (lane == 0) {
+      stack[0] = 0;
     }
-    const int nch = __builtin_popcount(kids);
-    int tot;
-    const int incl = wave_incl_scan(nch, &tot);
-    if (tail + tot > kBBStack) {
-      over = true;
-      break;
-    }
-    wave_lds_fence();  // this step's pops are read before the pushes overwrite them
-    int off = tail + incl - nch;
-    uint32_t kk = kids;
-    while (kk) {
-      const uint32_t o = (uint32_t)__builtin_ctz(kk);
-      kk &= kk - 1u;
-      stack[off++] = topo.x + __builtin_popcount((meta & 0xffu) & ((1u << o) - 1u));
-    }
-    tail += tot;
-    const double gb = wave_min_d(best);
-    const double t2 = gb * (1.0 + kFastPrune);
-    thr = t2 < thr ? t2 : thr;
-    ++steps;
+    over = false;
+    ++passes;
     wave_lds_fence();
+    while (tail > 0) {
+      const int batch = tail < 64 ? tail : 64;
+      const bool has = lane < batch;
+      const int32_t nid = has ? stack[tail - batch + lane] : 0;
+      tail -= batch;
+      const NodeRec* rr = a.nodes + nid;
+      const double2 l01 = *reinterpret_cast<const double2*>(&rr->lo[0]);
+      const double2 l2h0 = *reinterpret_cast<const double2*>(&rr->lo[2]);
+      const double2 h12 = *reinterpret_cast<const double2*>(&rr->hi[1]);
+      const int2 topo = *reinterpret_cast<const int2*>(&rr->first);
+      const uint32_t meta = (uint32_t)topo.y;
+      // pushed against an older (larger) bound: test the node itself again
+      const bool live = has && !(box_s(l01.x, l01.y, l2h0.x, l2h0.y, h12.x, h12.y, qx, qy, qz) > thr);
+      uint32_t kids = 0;
+      if (live && (meta & kLeafBit)) {
+        const int32_t cnt = (int32_t)(meta & ~kLeafBit);
+        for (int32_t k = 0; k < cnt; k++) {
+          const TgtPt* p = a.pts + topo.x + k;
+          const double2 pxy = *reinterpret_cast<const double2*>(&p->x);
+          const double dx = pxy.x - qx, dy = pxy.y - qy, dz = p->z - qz;
+          const double d2 = dx * dx + dy * dy + dz * dz;
+          if (d2 < best) {
+            second = best;
+            best = d2;
+            bpos = topo.x + k;
+          } else if (d2 < second) {
+            second = d2;
+          }
+        }
+      } else if (live) {
+        kids = children_in_ball(rr, meta & 0xffu, qx, qy, qz, thr);
+      }
+      const int nch = __builtin_popcount(kids);
+      int tot;
+      const int incl = wave_incl_scan(nch, &tot);
+      if (tail + tot > kBBStack) {
+        over = true;
+        break;
+      }
+      wave_lds_fence();  // this step's pops are read before the pushes overwrite them
+      int off = tail + incl - nch;
+      uint32_t kk = kids;
+      while (kk) {
+        const uint32_t o = (uint32_t)__builtin_ctz(kk);
+        kk &= kk - 1u;
+        stack[off++] = topo.x + __builtin_popcount((meta & 0xffu) & ((1u << o) - 1u));
+      }
+      tail += tot;
+      const double gb = wave_min_d(best);
+      const double t2 = gb * (1.0 + kFastPrune);
+      thr = t2 < thr ? t2 : thr;
+      ++steps;
+      wave_lds_fence();
+    }
+    wave_lds_fence();
+    // again with the tighter bound (thr holds the best so far), while it shrinks
+    if (!over || passes >= kBBPasses || !(thr < thr0)) break;
   }
-  wave_lds_fence();
   if (a.dbg && lane == 0) {
     atomicAdd(&a.dbg[27], 1ull);
     atomicAdd(&a.dbg[28], (unsigned long long)steps);
+    if (over) atomicAdd(&a.dbg[23], 1ull);
   }
   if (over) return false;
   // the wave's best, and its second: the smallest of the other lanes' bests and the best lane's
@@ -1453,7 +1478,8 @@ __global__ void __launch_bounds__(64) k_nn_ball(NNLaunch a) {
       qu = found < qu ? found : qu;
     }
     wave_lds_fence();
-    if (a.dbg && lane == 0) atomicAdd(&a.dbg[29], (unsigned long long)__popcll(__ballot(handed)));
+    const unsigned long long handed_m = __ballot(handed);
+    if (a.dbg && lane == 0) atomicAdd(&a.dbg[29], (unsigned long long)__popcll(handed_m));
     for (unsigned long long hm = __ballot(handed); hm; hm &= hm - 1) {
       const int k = __builtin_ctzll(hm);
       const int64_t iq = __builtin_amdgcn_readlane(e, k) & 0x3fffffff;

@@ -28,19 +28,20 @@ tgt, src, _ = icp.synth_scene(n, **kw)
 with icp.Context(0, icp.config(debug_counters=1, timing_stride=1, **cfg)) as ctx:
     ctx.set_target(tgt, 10, 20, icp.RULES_ENGINE)
     ctx.set_source(src)
-    T = None
+    # the engine's own loop (icp_session_step: the reference's increments and stops)
+    sess = ctx.session(icp.params_default(max_iterations=iters, tolerance=0.0, flags=icp.FLAG_NO_EARLY_STOP))
     for it in range(iters):
         t0 = time.perf_counter()
-        st = ctx.iterate(T, it, icp.RULES_ENGINE, 3.0)
+        rec = sess.step()
         wall = (time.perf_counter() - t0) * 1e3
         c = ctx.debug_counters()
         nn_ms, it_ms = ctx.last_timing()
         out = {"it": it, "wall_ms": round(wall, 3), "search_ms": round(nn_ms, 4), "iter_ms": round(it_ms, 4),
-               "ball": st.n_ball_search, "lane": st.n_lane_search, "exact": st.n_fallback, "valid": st.valid,
-               "rmse": st.rmse}
+               "rmse": None if rec is None else rec.rmse}
         for k in ("waves", "overflow_waves", "not_joined", "not_covered", "ball_overflow", "ball_points",
                   "fp64_scan_waves", "cache_hits", "scan_pairs", "staged_points", "bb_queries", "bb_steps",
-                  "lane_handed"):
+                  "lane_handed", "bb_overflow"):
             out[k] = c.get(k)
         print(json.dumps(out), flush=True)
-        T = icp.best_fit_from_stats(st)
+    sess.finish()
+    sess.close()
