@@ -15,7 +15,7 @@ the resident source + exact octree NN + residual + 3-sigma statistics (RCCL all-
 Rank 0 prints ONE JSON line. `value` = the points of all ranks x K / the wall time of the K timed
 iterations (max over ranks); `median` = the same rate from the median iteration of 2..K
 (SURVEY.md §8d). Extra objects:
-  roofline      the search kernel k_nn_wave: its compulsory HBM bytes per launch (DESIGN.md §5:
+  roofline      the search kernel k_nn_wave: its compulsory HBM bytes per launch (DESIGN.md §3.1:
                 64 B per query streamed + every target point (28 B) and node (56 B) once) / its
                 average HIP-event duration over the timed iterations; `traffic` = PMC bytes per
                 launch (rocprofv3, calibrated per access width: tools/calib_pmc.sh) of the same
@@ -60,7 +60,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
 # BASELINE.json configs by cloud size (config 3 is the LAS pair: tests/test_gpu_lasflow.py)
 CONFIG_NAMES = {100_000: "config2", 1_000_000: "synthetic-1M (config 3's size; config 3 itself, the LAS flow, is tests/test_gpu_lasflow.py)", 10_000_000: "config4", 50_000_000: "config5"}
 SEARCH_SOURCES = ("nn_kernels.hip", "nn_device.h", "kernels.h", "wave_stats.h")
-# compulsory bytes of one k_nn_wave<true> launch (DESIGN.md §5)
+# compulsory bytes of one k_nn_wave<true> launch (DESIGN.md §3.1)
 STREAM_B_PER_QUERY = 24 + 24 + 4 + 4 + 8  # source read + transformed write, previous match (guess), pos + dist
 TGT_B_PER_POINT = 28  # x, y, z + original index of a leaf-ordered target point
 NODE_B = 56  # box (48 B) + topology (8 B) of a node record
