@@ -1311,6 +1311,9 @@ __device__ __forceinline__ bool lane_query(const NNLaunch& a, int64_t i, unsigne
 // together, so the longest one sets its time: the budget bounds that, and the cooperative search
 // (64 nodes a step) takes the rest. Measured (profiles/r21/ab_lane_budget.txt, scene 20/5): 768
 // -> 64 visits: 1M 320 -> 635 Mcorr/s, 10M 600 -> 677; config 4 and config 3 unchanged.
+#ifndef ICP_BALL_DIRECT
+#define ICP_BALL_DIRECT 3  // k_nn_ball's direct mode: 0 never, 1 short lists, 2 always, 3 short or long
+#endif
 #ifndef ICP_LANE_BUDGET
 #define ICP_LANE_BUDGET 64
 #endif
@@ -1493,6 +1496,26 @@ __global__ void __launch_bounds__(64) k_nn_ball(NNLaunch a) {
     wave_lds_fence();
   };
   const unsigned cnt = a.fb_count[1];
+  // Direct mode: each wave takes whole queries, one after the other, with all its lanes: the
+  // cooperative search started from the cell tables of the query's bound (a few 64-node steps
+  // instead of the 16-lane ball walk and the follow-ups after it). Used for a short list (at most
+  // one query per wave of the launch: the steady state of a dense cloud, ~7.5k of 10M) and for a
+  // long one (over four per wave: an unconverged registration on surface data, where most balls
+  // overflow); the four-queries-per-wave ball walk keeps the lists in between, whose queries are
+  // mostly easy. Measured (profiles/r21/ab_ball_direct.txt): scene 10M 678 -> 1215 Mcorr/s,
+  // scene 1M 624 -> 1254 (driver window), config 4 unchanged; direct at every size cost config
+  // 4's window 4 % (its 15k-query lists of easy balls).
+  if (ICP_BALL_DIRECT == 2 || (ICP_BALL_DIRECT == 1 && cnt <= gridDim.x) ||
+      (ICP_BALL_DIRECT == 3 && (cnt <= gridDim.x || cnt > 4u * gridDim.x))) {
+    for (unsigned j = blockIdx.x; j < cnt; j += gridDim.x) {
+      const int64_t i = a.fb_list2[j];
+      const double u = a.fb_u2[j];
+      if (!wave_bb(a, i, u, reinterpret_cast<int32_t*>(lds_raw), lds_raw, lane) && lane == 0)
+        exact_query(a, i, lds_raw, 1);
+      wave_lds_fence();
+    }
+    return;
+  }
   for (unsigned j0 = blockIdx.x * kBallGroups; j0 < cnt; j0 += gridDim.x * kBallGroups) {
     const unsigned j = j0 + g;
     bool live = j < cnt;  // group-uniform
