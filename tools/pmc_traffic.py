@@ -39,11 +39,17 @@ def rows(pattern):
 
 
 def per_dispatch(prof, sub):
+    """Per-dispatch averages of the search kernel's counters over the dispatches of the profiled
+    workload: the largest grid (the context's process warm-up runs the same kernel on a 4096-point
+    pair first, icp_ctx.hip warm_kernels; those dispatches are left out)."""
+    rs = [r for r in rows(f"{prof}/{sub}/**/*counter_collection.csv") if KERNEL in r.get("Kernel_Name", "")]
+    if not rs:
+        return {}
+    gmax = max(int(r["Grid_Size"]) for r in rs)
     vals = defaultdict(lambda: defaultdict(float))
-    for r in rows(f"{prof}/{sub}/**/*counter_collection.csv"):
-        if KERNEL not in r.get("Kernel_Name", ""):
-            continue
-        vals[r["Counter_Name"]][r["Dispatch_Id"]] += float(r["Counter_Value"])
+    for r in rs:
+        if int(r["Grid_Size"]) == gmax:
+            vals[r["Counter_Name"]][r["Dispatch_Id"]] += float(r["Counter_Value"])
     return {k: (sum(v.values()) / len(v), len(v)) for k, v in vals.items() if v}
 
 
@@ -53,13 +59,15 @@ def main():
     sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
     from bench import search_source_sha1
     out = {"kernel": KERNEL, "n": n, "world": world, "search_src_sha1": search_source_sha1()}
-    stats = rows(f"{prof}/trace/**/*kernel_stats.csv")
-    for r in stats:
-        if KERNEL in r.get("Name", r.get("KernelName", "")):
-            out["trace_calls"] = int(r["Calls"])
-            out["trace_avg_ms"] = float(r["AverageNs"]) / 1e6
-            out["trace_min_ms"] = float(r["MinNs"]) / 1e6
-            out["trace_max_ms"] = float(r["MaxNs"]) / 1e6
+    # the kernel's durations over the profiled workload's dispatches (largest grid; see per_dispatch)
+    tr = [r for r in rows(f"{prof}/trace/**/*kernel_trace.csv") if KERNEL in r.get("Kernel_Name", "")]
+    if tr:
+        gmax = max(int(r["Grid_Size_X"]) for r in tr)
+        d = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in tr if int(r["Grid_Size_X"]) == gmax]
+        out["trace_calls"] = len(d)
+        out["trace_avg_ms"] = sum(d) / len(d)
+        out["trace_min_ms"] = min(d)
+        out["trace_max_ms"] = max(d)
     fetch = per_dispatch(prof, "pmc_fetch").get("FETCH_SIZE")
     write = per_dispatch(prof, "pmc_write").get("WRITE_SIZE")
     hits = per_dispatch(prof, "pmc_l2")
