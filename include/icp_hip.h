@@ -144,7 +144,14 @@ typedef struct icp_hip_config {
                               loads a kernel's code and sizes its scratch at the kernel's first
                               launch, which otherwise lands in the first real iterate (+1.3 ms
                               at 10M); 1: no warm-up                                     dflt 0 */
-  int32_t reserved[5];     /* zero (fields of later versions of this header)                    */
+  int32_t ball_mode;       /* k_nn_ball, the queries the wave search left: 0 a whole query per wave
+                              (the cooperative search from the cell tables of its bound) when the
+                              list is short (<= one per wave of the launch) or long (> four per
+                              wave: an unconverged registration on surface data), else four
+                              queries per wave (16-lane ball walks, follow-ups for the balls that
+                              overflow); 1 always the ball walk; 2 always whole queries. The same
+                              results either way                          dflt 0 */
+  int32_t reserved[4];     /* zero (fields of later versions of this header)                    */
   uint32_t config_version; /* ICP_HIP_CONFIG_VERSION, set by icp_hip_config_default; create_ex
                               rejects any other value (a struct from another header version)     */
 } icp_hip_config;

@@ -73,7 +73,7 @@ class HipConfig(C.Structure):
         ("candidate_margin", C.c_int32), ("certify_prev", C.c_int32), ("query_order", C.c_int32),
         ("overflow_halves", C.c_int32), ("device_loop", C.c_int32), ("timing_stride", C.c_int32),
         ("candidate_loose", C.c_int32), ("candidate_lead", C.c_int32), ("fused_cull", C.c_int32),
-        ("peer_timeout_ms", C.c_int32), ("no_warmup", C.c_int32), ("reserved", C.c_int32 * 5), ("config_version", C.c_uint32),
+        ("peer_timeout_ms", C.c_int32), ("no_warmup", C.c_int32), ("ball_mode", C.c_int32), ("reserved", C.c_int32 * 4), ("config_version", C.c_uint32),
     ]
 
 

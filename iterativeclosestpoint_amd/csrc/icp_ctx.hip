@@ -123,6 +123,7 @@ static NNLaunch base_launch(const icp_hip_ctx* c) {
   a.cells = c->cells;
   a.cell_lmax = c->cell_lmax;
   a.join_factor = c->cfg.join_factor;
+  a.ball_mode = c->cfg.ball_mode;
   a.xcd_blocks = c->cfg.xcd_blocks;
   a.scan_groups = c->cfg.scan_groups;
   a.certify_prev = c->cfg.certify_prev;
@@ -147,7 +148,7 @@ static void warm_kernels(int device, const icp_hip_config& conf) {
   const uint64_t key = (uint64_t)conf.search | (uint64_t)conf.scan_groups << 4 | (uint64_t)conf.certify_prev << 8 |
                        (uint64_t)(conf.debug_counters != 0) << 12 | (uint64_t)conf.fused_cull << 13 |
                        (uint64_t)conf.overflow_halves << 14 | (uint64_t)conf.scan32 << 15 |
-                       (uint64_t)conf.candidate_cache << 16;
+                       (uint64_t)conf.candidate_cache << 16 | (uint64_t)conf.ball_mode << 17;
   std::lock_guard<std::mutex> lk(mu);
   for (const auto& d : done)
     if (d.first == device && d.second == key) return;
@@ -217,6 +218,7 @@ int icp_hip_create_ex(icp_hip_ctx** out, int device, const icp_hip_config* cfg) 
                                 "of this header)");
   if (conf.peer_timeout_ms < 0) return fail(ICP_HIP_EINVAL, "config: peer_timeout_ms must be >= 0");
   if (conf.no_warmup != 0 && conf.no_warmup != 1) return fail(ICP_HIP_EINVAL, "config: no_warmup must be 0 or 1");
+  if (conf.ball_mode < 0 || conf.ball_mode > 2) return fail(ICP_HIP_EINVAL, "config: ball_mode out of [0, 2]");
   if (conf.search != ICP_SEARCH_CERTIFIED && conf.search != ICP_SEARCH_REFERENCE)
     return fail(ICP_HIP_EINVAL, "config: unknown search");
   if (conf.octree_builder != ICP_BUILD_AUTO && conf.octree_builder != ICP_BUILD_HOST)

@@ -119,6 +119,7 @@ struct NNLaunch {
   WaveStat* wstat;          // per-wave covariance records (null: none; the cull pass does it all)
   const IterDev* fz;        // the band of this iterate (IterDev::fz_*)
   int32_t ball_queue_off;   // k_nn_ball: byte offset of its follow-up queue in LDS
+  int32_t ball_mode;        // icp_hip_config.ball_mode (k_nn_ball's direct mode)
 };
 
 // Threads per block of the per-thread search kernels for a given stack depth.

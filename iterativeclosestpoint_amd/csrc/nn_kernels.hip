@@ -1311,9 +1311,6 @@ __device__ __forceinline__ bool lane_query(const NNLaunch& a, int64_t i, unsigne
 // together, so the longest one sets its time: the budget bounds that, and the cooperative search
 // (64 nodes a step) takes the rest. Measured (profiles/r21/ab_lane_budget.txt, scene 20/5): 768
 // -> 64 visits: 1M 320 -> 635 Mcorr/s, 10M 600 -> 677; config 4 and config 3 unchanged.
-#ifndef ICP_BALL_DIRECT
-#define ICP_BALL_DIRECT 3  // k_nn_ball's direct mode: 0 never, 1 short lists, 2 always, 3 short or long
-#endif
 #ifndef ICP_LANE_BUDGET
 #define ICP_LANE_BUDGET 64
 #endif
@@ -1505,8 +1502,8 @@ __global__ void __launch_bounds__(64) k_nn_ball(NNLaunch a) {
   // mostly easy. Measured (profiles/r21/ab_ball_direct.txt): scene 10M 678 -> 1215 Mcorr/s,
   // scene 1M 624 -> 1254 (driver window), config 4 unchanged; direct at every size cost config
   // 4's window 4 % (its 15k-query lists of easy balls).
-  if (ICP_BALL_DIRECT == 2 || (ICP_BALL_DIRECT == 1 && cnt <= gridDim.x) ||
-      (ICP_BALL_DIRECT == 3 && (cnt <= gridDim.x || cnt > 4u * gridDim.x))) {
+  // (icp_hip_config.ball_mode: 0 this rule, 1 the ball walk always, 2 direct always)
+  if (a.ball_mode == 2 || (a.ball_mode == 0 && (cnt <= gridDim.x || cnt > 4u * gridDim.x))) {
     for (unsigned j = blockIdx.x; j < cnt; j += gridDim.x) {
       const int64_t i = a.fb_list2[j];
       const double u = a.fb_u2[j];

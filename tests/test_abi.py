@@ -66,7 +66,8 @@ def test_create_ex_validates_config_without_a_gpu(icp):
     h = C.c_void_p()
     cfg = icp.config()
     assert cfg.no_warmup == 0 and cfg.config_version == 2
-    for field, bad in (("no_warmup", 2), ("peer_timeout_ms", -1), ("scan_groups", 3), ("config_version", 1)):
+    for field, bad in (("no_warmup", 2), ("ball_mode", 3), ("peer_timeout_ms", -1), ("scan_groups", 3),
+                       ("config_version", 1)):
         c = icp.config()
         setattr(c, field, bad)
         assert L.icp_hip_create_ex(C.byref(h), 0, C.byref(c)) == icp.EINVAL, field

@@ -63,3 +63,35 @@ def test_scene_registration_vs_oracle(icp, oracle, scene):
     # the registration moves towards the known pose (5 iterates of a 2 deg / 0.36 m offset)
     err0 = np.abs(np.eye(4) - T_true)[:3, 3].max()
     assert np.abs(T - T_true)[:3, 3].max() < err0
+
+
+@pytest.mark.parametrize("which", ["scene", "blob"])
+def test_ball_modes_agree(icp, oracle, scene, which):
+    """k_nn_ball's two ways through the queries the wave search left (config.ball_mode: 1 the
+    four-per-wave ball walk with its follow-ups, 2 a whole query per wave by the cooperative
+    search, 0 the size rule between them): the same correspondences, residuals and statistics bit
+    for bit over the first iterates (long lists of far queries on the scene, short ones on the
+    blob), and the oracle's on the last one."""
+    if which == "scene":
+        tgt, src, _ = scene
+    else:
+        tgt, src, _ = icp.synth_pair(300_000, yaw_deg=3.0)
+    out = {}
+    for mode in (0, 1, 2):
+        with icp.Context(0, icp.config(ball_mode=mode)) as ctx:
+            ctx.set_target(tgt, 10, 20, icp.RULES_ENGINE)
+            ctx.set_source(src)
+            T, recs = None, []
+            for it in range(3):
+                st = ctx.iterate(T, it, icp.RULES_ENGINE, 3.0)
+                recs.append((st.valid, st.mean, st.std, st.rmse, tuple(st.H)))
+                T = icp.best_fit_from_stats(st)
+            idx, d = ctx.get_correspondences()
+            out[mode] = (recs, idx, d, ctx.get_source())
+    for mode in (1, 2):
+        assert out[mode][0] == out[0][0]
+        for k in (1, 2, 3):
+            np.testing.assert_array_equal(out[mode][k], out[0][k])
+    oidx, od = oracle.OracleTree(tgt).nn(out[0][3], init_best=oracle.DBL_MAX)
+    np.testing.assert_array_equal(out[0][1], oidx)
+    np.testing.assert_array_equal(out[0][2], od)
