@@ -504,7 +504,9 @@ def main() -> int:
             "median": {"iter_ms": round(med_ms, 4), "value": round(n / med_ms / 1e3, 3),
                        "over": f"iterations 2..{args.steps} of the timed region (host wall per step, max over ranks)"},
             "first_iteration": {"ms": round(float(first_ms[0]), 4), "search_kernel_ms": round(float(first_nn_ms[0]), 4),
-                                "note": "no previous residuals: the guess is a descent, the search kernel is k_nn_wave<false>"},
+                                "note": "no previous matches: the guesses are a descent, its sibling leaves and the other lanes' "
+                                        "points (k_nn_wave<false>), every wave walks, full cull pass; kernels loaded by the "
+                                        "context's process warm-up (icp_hip_config.no_warmup)"},
             # ranks sharing one GPU (host-exchange rehearsal) contend for it: no per-rank roofline
             "roofline": None if shared_gpu else {
                 "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
