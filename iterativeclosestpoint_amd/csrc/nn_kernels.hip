@@ -230,7 +230,11 @@ static_assert(kStatLds <= kWaveLds, "the record's reduction fits the wave's LDS 
 #ifndef ICP_GUESS_LANES
 #define ICP_GUESS_LANES 64  // lanes sharing their first-iterate guess points (16, 32, 64)
 #endif
-template <bool APPLY, int NG, bool CERT, bool HALF, bool DBG>
+// WC: the instance of an iterate with the candidate cache and previous residuals (every wave that
+// joins either reuses its record or walks and stores one): a walking wave stores its entries
+// before the scan and then streams them back as a reusing wave does, so the instance carries one
+// scan path (ICP_WALK_STREAM).
+template <bool APPLY, int NG, bool CERT, bool HALF, bool DBG, bool WC = false>
 __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, const int lane, unsigned char* wl) {
   constexpr bool kDbg = DBG && kDbgCounts;
   static_assert(NG == 1 || NG == 2 || NG == 4, "scan groups: 1, 2 or 4");
@@ -790,6 +794,46 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
   // gathers the points of its list and, with the cache, stores those inside B+).
   double best = __builtin_inf(), second = __builtin_inf();
   int32_t bpos = -1;
+  // streamed: the candidates are cache entries (a reusing wave's, or in the WC instance the ones a
+  // walking wave stores here: the points of its list inside B+, in list order, before the scan)
+  bool streamed = reuse;
+  if constexpr (WC) {
+    if (wstore) {
+      int wcount = 0;
+      double4 nxtp = make_double4(0.0, 0.0, 0.0, 0.0);
+      if (lane < nleaf) {
+        const int32_t g = plist[lane];
+        const TgtPt* p = a.pts + g;
+        const double2 xy = *reinterpret_cast<const double2*>(&p->x);
+        nxtp = make_double4(xy.x, xy.y, p->z, __longlong_as_double((long long)g));
+      }
+      for (int base = 0; base < nleaf; base += 64) {
+        const double4 cur = nxtp;
+        const int nb = base + 64;
+        if (nb + lane < nleaf) {
+          const int32_t g = plist[nb + lane];
+          const TgtPt* p = a.pts + g;
+          const double2 xy = *reinterpret_cast<const double2*>(&p->x);
+          nxtp = make_double4(xy.x, xy.y, p->z, __longlong_as_double((long long)g));
+        }
+        const bool inp = base + lane < nleaf && cur.x >= wlx && cur.x <= whx && cur.y >= wly && cur.y <= why &&
+                         cur.z >= wlz && cur.z <= whz;
+        const unsigned long long pm = __ballot(inp);
+        if (inp)
+          wents[wcount + mask_rank(pm)] = make_float4((float)(cur.x - ocx), (float)(cur.y - ocy), (float)(cur.z - ocz),
+                                                      __int_as_float((int)__double_as_longlong(cur.w)));
+        wcount += __popcll(pm);
+      }
+      store_header(wcount);
+      wstore = false;
+      nleaf = wcount;
+      // the wave's own stores, read back by other lanes of the wave (same CU: no L1 invalidate)
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      ent0 = lane < wcount ? wents[lane] : make_float4(0.f, 0.f, 0.f, 0.f);
+      streamed = true;
+    }
+  }
   const int npts = nleaf;
   int scanned_pts = 0;
   bool need64 = __ballot(join) != 0 && npts > 0;
@@ -801,7 +845,7 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
       // stages up to 64 points per group (NG x 1 KB: the stack area and the list area) across its
       // chunks and scans once they would overflow (usually once per wave); slots stay below 64
       // (6 key bits)
-      const int SP = reuse ? 64 : LG;
+      const int SP = streamed ? 64 : LG;
       const int gq = lane / LG;  // this lane's group
       // staging area: NG segments of SP points, in pairs [x0 x1 y0 y1 z0 z1 w0 w1] (32 B) so that
       // one packed fp32 instruction (v_pk_add/mul/fma_f32) evaluates an axis of two points.
@@ -926,7 +970,7 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
         }
       };
       wave_lds_fence();
-      if (reuse) {
+      if (WC || streamed) {
         // Accumulate: each chunk's points are staged behind the previous chunks' (per group),
         // and a scan round runs only when a group's segment would overflow, and at the end. The
         // lockstep scan then pays max over groups of the wave's whole count once, not of every
@@ -1088,7 +1132,7 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
     double4 nxtp = make_double4(0.0, 0.0, 0.0, 0.0);
     bool nin = false;
     // candidate k: from the walk's list, or the id word of a reused cache entry
-    auto cand_id = [&](int k) { return reuse ? reinterpret_cast<const int32_t*>(wents + k)[3] : plist[k]; };
+    auto cand_id = [&](int k) { return (WC || streamed) ? reinterpret_cast<const int32_t*>(wents + k)[3] : plist[k]; };
     if (lane < npts) {
       const int32_t g = cand_id(lane);
       const TgtPt* p = a.pts + g;
@@ -1220,13 +1264,22 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
 #ifndef ICP_WAVE_WPE
 #define ICP_WAVE_WPE 7
 #endif
-template <bool APPLY, int NG, bool CERT, bool DBG>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ICP_WAVE_WPE, ICP_WAVE_WPE))) k_nn_wave(NNLaunch a) {
+#ifndef ICP_WAVE_WPE_WC
+#define ICP_WAVE_WPE_WC ICP_WAVE_WPE
+#endif
+// The WC instance (walking waves store their entries first, one scan path): 69 VGPRs and no
+// scratch at 7 waves; search 0.473-0.477 -> 0.456-0.457 ms over 200 steps at 10M
+// (profiles/r21/ab_walk_stream.txt). At 8 waves it spills 24 B and runs 0.49.
+#ifndef ICP_WALK_STREAM
+#define ICP_WALK_STREAM 1
+#endif
+template <bool APPLY, int NG, bool CERT, bool DBG, bool WC>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WC ? ICP_WAVE_WPE_WC : ICP_WAVE_WPE, WC ? ICP_WAVE_WPE_WC : ICP_WAVE_WPE))) k_nn_wave(NNLaunch a) {
   if (a.loop && a.loop->core.done) return;  // the device loop's session finished
   extern __shared__ __attribute__((aligned(16))) unsigned long long lds_raw[];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int32_t i = (int32_t)(xcd_block((unsigned)a.xcd_blocks) * blockDim.x + threadIdx.x);  // n <= INT32_MAX
-  wave_search<APPLY, NG, CERT, false, DBG>(a, i, lane, reinterpret_cast<unsigned char*>(lds_raw) + wv * kWaveLds);
+  wave_search<APPLY, NG, CERT, false, DBG, WC>(a, i, lane, reinterpret_cast<unsigned char*>(lds_raw) + wv * kWaveLds);
 }
 
 // The half pass: every wave takes 32-query halves of overflowed waves from the list (grid-stride;
@@ -1832,13 +1885,18 @@ hipError_t launch_nn(const NNLaunch& a, hipStream_t s) {
   // instances: transform, scan groups, certificate, debug counters
   auto pick = [&](auto cert_c, auto dbg_c) -> hipError_t {
     constexpr bool C = decltype(cert_c)::value, D = decltype(dbg_c)::value;
-    switch ((a.apply ? 8 : 0) + a.scan_groups) {
-      case 9: wave(k_nn_wave<true, 1, C, D>); break;
-      case 10: wave(k_nn_wave<true, 2, C, D>); break;
-      case 12: wave(k_nn_wave<true, 4, C, D>); break;
-      case 1: wave(k_nn_wave<false, 1, C, D>); break;
-      case 2: wave(k_nn_wave<false, 2, C, D>); break;
-      case 4: wave(k_nn_wave<false, 4, C, D>); break;
+    // the cache instance where every joined wave reuses or stores (an iterate after a search)
+    const bool wc = ICP_WALK_STREAM && a.apply && a.wc_box != nullptr && a.have_prev;
+    switch ((wc ? 16 : 0) + (a.apply ? 8 : 0) + a.scan_groups) {
+      case 25: wave(k_nn_wave<true, 1, C, D, true>); break;
+      case 26: wave(k_nn_wave<true, 2, C, D, true>); break;
+      case 28: wave(k_nn_wave<true, 4, C, D, true>); break;
+      case 9: wave(k_nn_wave<true, 1, C, D, false>); break;
+      case 10: wave(k_nn_wave<true, 2, C, D, false>); break;
+      case 12: wave(k_nn_wave<true, 4, C, D, false>); break;
+      case 1: wave(k_nn_wave<false, 1, C, D, false>); break;
+      case 2: wave(k_nn_wave<false, 2, C, D, false>); break;
+      case 4: wave(k_nn_wave<false, 4, C, D, false>); break;
       default: return hipErrorInvalidValue;
     }
     return hipSuccess;
