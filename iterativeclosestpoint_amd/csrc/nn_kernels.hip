@@ -230,11 +230,12 @@ static_assert(kStatLds <= kWaveLds, "the record's reduction fits the wave's LDS 
 #ifndef ICP_GUESS_LANES
 #define ICP_GUESS_LANES 64  // lanes sharing their first-iterate guess points (16, 32, 64)
 #endif
-// WC: the instance of an iterate with the candidate cache and previous residuals (every wave that
-// joins either reuses its record or walks and stores one): a walking wave stores its entries
-// before the scan and then streams them back as a reusing wave does, so the instance carries one
-// scan path (ICP_WALK_STREAM).
-template <bool APPLY, int NG, bool CERT, bool HALF, bool DBG, bool WC = false>
+// CM, the candidate-cache instance: 1 (WC) an iterate with the cache and previous residuals (every
+// wave that joins either reuses its record or walks and stores one): a walking wave stores its
+// entries before the scan and then streams them back as a reusing wave does, so the instance
+// carries one scan path (ICP_WALK_STREAM); 2 (NC) a first iterate without a transform (no record
+// is reused or stored: the instance carries no cache code); 0 either.
+template <bool APPLY, int NG, bool CERT, bool HALF, bool DBG, int CM = 0>
 __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, const int lane, unsigned char* wl) {
   constexpr bool kDbg = DBG && kDbgCounts;
   static_assert(NG == 1 || NG == 2 || NG == 4, "scan groups: 1, 2 or 4");
@@ -249,7 +250,7 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
   // reusing wave has its first chunk before the box is known; unused otherwise).
   const int32_t i0 = __builtin_amdgcn_readfirstlane(i);
   const uint32_t wid = (uint32_t)i0 >> 6;
-  const bool use_wc = !HALF && a.wc_box != nullptr && i0 < a.n;
+  const bool use_wc = !HALF && CM != 2 && a.wc_box != nullptr && i0 < a.n;
   // the previous match, whose fl(d2) is u (read unconditionally: an unused load costs no wait,
   // while a conditional one is waited for inside its branch)
   const int32_t prev_pos = qat(a.pos_out, active ? i : 0);
@@ -797,7 +798,7 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
   // streamed: the candidates are cache entries (a reusing wave's, or in the WC instance the ones a
   // walking wave stores here: the points of its list inside B+, in list order, before the scan)
   bool streamed = reuse;
-  if constexpr (WC) {
+  if constexpr (CM == 1) {
     if (wstore) {
       int wcount = 0;
       double4 nxtp = make_double4(0.0, 0.0, 0.0, 0.0);
@@ -970,7 +971,7 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
         }
       };
       wave_lds_fence();
-      if (WC || streamed) {
+      if (CM == 1 || streamed) {
         // Accumulate: each chunk's points are staged behind the previous chunks' (per group),
         // and a scan round runs only when a group's segment would overflow, and at the end. The
         // lockstep scan then pays max over groups of the wave's whole count once, not of every
@@ -1132,7 +1133,7 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
     double4 nxtp = make_double4(0.0, 0.0, 0.0, 0.0);
     bool nin = false;
     // candidate k: from the walk's list, or the id word of a reused cache entry
-    auto cand_id = [&](int k) { return (WC || streamed) ? reinterpret_cast<const int32_t*>(wents + k)[3] : plist[k]; };
+    auto cand_id = [&](int k) { return (CM == 1 || streamed) ? reinterpret_cast<const int32_t*>(wents + k)[3] : plist[k]; };
     if (lane < npts) {
       const int32_t g = cand_id(lane);
       const TgtPt* p = a.pts + g;
@@ -1267,19 +1268,25 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
 #ifndef ICP_WAVE_WPE_WC
 #define ICP_WAVE_WPE_WC ICP_WAVE_WPE
 #endif
+#ifndef ICP_WAVE_WPE_NC
+#define ICP_WAVE_WPE_NC ICP_WAVE_WPE
+#endif
 // The WC instance (walking waves store their entries first, one scan path): 69 VGPRs and no
 // scratch at 7 waves; search 0.473-0.477 -> 0.456-0.457 ms over 200 steps at 10M
 // (profiles/r21/ab_walk_stream.txt). At 8 waves it spills 24 B and runs 0.49.
 #ifndef ICP_WALK_STREAM
 #define ICP_WALK_STREAM 1
 #endif
-template <bool APPLY, int NG, bool CERT, bool DBG, bool WC>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WC ? ICP_WAVE_WPE_WC : ICP_WAVE_WPE, WC ? ICP_WAVE_WPE_WC : ICP_WAVE_WPE))) k_nn_wave(NNLaunch a) {
+#ifndef ICP_FIRST_NC
+#define ICP_FIRST_NC 1
+#endif
+template <bool APPLY, int NG, bool CERT, bool DBG, int CM>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CM == 1 ? ICP_WAVE_WPE_WC : CM == 2 ? ICP_WAVE_WPE_NC : ICP_WAVE_WPE, CM == 1 ? ICP_WAVE_WPE_WC : CM == 2 ? ICP_WAVE_WPE_NC : ICP_WAVE_WPE))) k_nn_wave(NNLaunch a) {
   if (a.loop && a.loop->core.done) return;  // the device loop's session finished
   extern __shared__ __attribute__((aligned(16))) unsigned long long lds_raw[];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int32_t i = (int32_t)(xcd_block((unsigned)a.xcd_blocks) * blockDim.x + threadIdx.x);  // n <= INT32_MAX
-  wave_search<APPLY, NG, CERT, false, DBG, WC>(a, i, lane, reinterpret_cast<unsigned char*>(lds_raw) + wv * kWaveLds);
+  wave_search<APPLY, NG, CERT, false, DBG, CM>(a, i, lane, reinterpret_cast<unsigned char*>(lds_raw) + wv * kWaveLds);
 }
 
 // The half pass: every wave takes 32-query halves of overflowed waves from the list (grid-stride;
@@ -1887,16 +1894,22 @@ hipError_t launch_nn(const NNLaunch& a, hipStream_t s) {
     constexpr bool C = decltype(cert_c)::value, D = decltype(dbg_c)::value;
     // the cache instance where every joined wave reuses or stores (an iterate after a search)
     const bool wc = ICP_WALK_STREAM && a.apply && a.wc_box != nullptr && a.have_prev;
-    switch ((wc ? 16 : 0) + (a.apply ? 8 : 0) + a.scan_groups) {
-      case 25: wave(k_nn_wave<true, 1, C, D, true>); break;
-      case 26: wave(k_nn_wave<true, 2, C, D, true>); break;
-      case 28: wave(k_nn_wave<true, 4, C, D, true>); break;
-      case 9: wave(k_nn_wave<true, 1, C, D, false>); break;
-      case 10: wave(k_nn_wave<true, 2, C, D, false>); break;
-      case 12: wave(k_nn_wave<true, 4, C, D, false>); break;
-      case 1: wave(k_nn_wave<false, 1, C, D, false>); break;
-      case 2: wave(k_nn_wave<false, 2, C, D, false>); break;
-      case 4: wave(k_nn_wave<false, 4, C, D, false>); break;
+    // the instance without the cache for a source's first iterate (its walking waves store
+    // nothing; a record is reused only after a search)
+    const bool nc = ICP_FIRST_NC && !a.apply && !a.have_prev;
+    switch ((wc ? 16 : 0) + (nc ? 32 : 0) + (a.apply ? 8 : 0) + a.scan_groups) {
+      case 25: wave(k_nn_wave<true, 1, C, D, 1>); break;
+      case 26: wave(k_nn_wave<true, 2, C, D, 1>); break;
+      case 28: wave(k_nn_wave<true, 4, C, D, 1>); break;
+      case 9: wave(k_nn_wave<true, 1, C, D, 0>); break;
+      case 10: wave(k_nn_wave<true, 2, C, D, 0>); break;
+      case 12: wave(k_nn_wave<true, 4, C, D, 0>); break;
+      case 33: wave(k_nn_wave<false, 1, C, D, 2>); break;
+      case 34: wave(k_nn_wave<false, 2, C, D, 2>); break;
+      case 36: wave(k_nn_wave<false, 4, C, D, 2>); break;
+      case 1: wave(k_nn_wave<false, 1, C, D, 0>); break;
+      case 2: wave(k_nn_wave<false, 2, C, D, 0>); break;
+      case 4: wave(k_nn_wave<false, 4, C, D, 0>); break;
       default: return hipErrorInvalidValue;
     }
     return hipSuccess;
