@@ -237,6 +237,8 @@ static_assert(kStatLds <= kWaveLds, "the record's reduction fits the wave's LDS 
 // is reused or stored: the instance carries no cache code); 0 either.
 template <bool APPLY, int NG, bool CERT, bool HALF, bool DBG, int CM = 0>
 __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, const int lane, unsigned char* wl) {
+  // previous residuals: known to the WC (yes) and NC (no) instances
+  const bool have_prev = CM == 1 ? true : CM == 2 ? false : a.have_prev != 0;
   constexpr bool kDbg = DBG && kDbgCounts;
   static_assert(NG == 1 || NG == 2 || NG == 4, "scan groups: 1, 2 or 4");
   static_assert(!(HALF && (APPLY || CERT)), "the half pass searches moved queries");
@@ -272,7 +274,7 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
   double u = __builtin_inf();
   int32_t gpos = -1;  // (first iterate) the target point whose distance is u
   bool safe = false;  // the previous match certified from its separation: no search
-  if (active && finite_q && a.have_prev) {
+  if (active && finite_q && have_prev) {
     // the previous match is a candidate: its fl(d2) from the moved query bounds the nearest
     // point's (usually well below (previous residual + displacement)^2)
     const TgtPt* pp = a.pts + prev_pos;
@@ -361,7 +363,7 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
   // and follow-up searches in the iterate with the loosest guesses. Measured at 10M (one MI355X,
   // profiles/r21/ab_first_iterate_guess.txt): lanes not joining their wave's box 14651 -> 1214,
   // overflowing waves 3546 -> 1075, first iterate 2.78 -> 2.52 ms (16 lanes: 2.61, 32: 2.58).
-  if (!APPLY && !a.have_prev) {
+  if (!APPLY && !have_prev) {
     constexpr int kGL = ICP_GUESS_LANES;
     const double rx = __shfl(qx, lane & (64 - kGL), kWave), ry = __shfl(qy, lane & (64 - kGL), kWave),
                  rz = __shfl(qz, lane & (64 - kGL), kWave);
@@ -398,7 +400,7 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
   //   2: certified lanes settle, the others search (join) as usual
   //   3: certified lanes settle; a wave left with at most kOpenToBall open queries sends them to
   //      the ball search (with u as their guess) and ends here, otherwise it searches them (2)
-  if (CERT && a.have_prev) {
+  if (CERT && have_prev) {
     const unsigned long long open = __ballot(active && !safe);
     if (kDbg && a.dbg) {
       const unsigned long long settled = __ballot(safe);  // every lane takes part in the ballot
@@ -673,7 +675,7 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
       // doubles are kept in scalar registers.
       // Without previous residuals (descent guesses: large, loose boxes that the next iterate
       // re-walks anyway) the wave walks B itself and stores nothing.
-      const bool keep = wb && a.have_prev;
+      const bool keep = wb && have_prev;
       const double m = keep ? a.wc_margin * 0.5 * dmax_(dmax_(bhx - blx, bhy - bly), bhz - blz) : 0.0;
       // The lead: the queries of a wave keep moving the same way for many iterates (ICP's
       // increments change slowly), so the stored B+ also covers where B will be after wc_lead
@@ -763,7 +765,7 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
   // balls; an overflowing half hands its queries to the ball search.
   bool deferred = false;
   if (overflow) {
-    if (!HALF && a.fb_list3 != nullptr) {
+    if (!HALF && CM != 1 && a.fb_list3 != nullptr) {  // the half pass: first iterates only
       // entries (half id, mask of its deferred lanes): the half pass searches exactly these
       const unsigned long long dm = __ballot(join);
       deferred = join;
