@@ -57,6 +57,10 @@ extern "C" {
 /* Explicit configuration of a context (nothing is read from the environment). Every setting
  * gives the same correspondences; they select how the device finds them. */
 typedef struct icp_hip_config {
+  uint32_t config_version; /* ICP_HIP_CONFIG_VERSION, set by icp_hip_config_default. The FIRST word,
+                              so create_ex checks it before it copies the struct: a struct of
+                              another header version (v1/v2 began with `search`, 0 or 1) is
+                              rejected without reading past the caller's object               */
   int32_t search;         /* ICP_SEARCH_*                                        default CERTIFIED */
   int32_t scan32;         /* 1: fp32 filter scan + fp64 certificate; 0: fp64 scan      default 1 */
   int32_t cell_starts;    /* 1: wave walks start from per-level cell tables; 0: root    default 1 */
@@ -151,11 +155,10 @@ typedef struct icp_hip_config {
                               queries per wave (16-lane ball walks, follow-ups for the balls that
                               overflow); 1 always the ball walk; 2 always whole queries. The same
                               results either way                          dflt 0 */
-  int32_t reserved[4];     /* zero (fields of later versions of this header)                    */
-  uint32_t config_version; /* ICP_HIP_CONFIG_VERSION, set by icp_hip_config_default; create_ex
-                              rejects any other value (a struct from another header version)     */
+  int32_t reserved[4];     /* zero (fields of later versions of this header); create_ex rejects
+                              a nonzero word                                                    */
 } icp_hip_config;
-#define ICP_HIP_CONFIG_VERSION 2u /* 1: r4 and earlier (no peer_timeout_ms, no version field) */
+#define ICP_HIP_CONFIG_VERSION 3u /* 1: r4 and earlier (no version field); 2: r5 (version last) */
 
 /* Slots of icp_hip_debug_counters (summed over the last iterate's search launches). */
 #define ICP_DBG_WAVES 0          /* waves of the wave search                                  */

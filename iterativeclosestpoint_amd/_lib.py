@@ -67,13 +67,13 @@ class IterStats(C.Structure):
 class HipConfig(C.Structure):
     """icp_hip_config (include/icp_hip.h): explicit search options of a context."""
     _fields_ = [
-        ("search", C.c_int32), ("scan32", C.c_int32), ("cell_starts", C.c_int32),
+        ("config_version", C.c_uint32), ("search", C.c_int32), ("scan32", C.c_int32), ("cell_starts", C.c_int32),
         ("octree_builder", C.c_int32), ("join_factor", C.c_double), ("debug_counters", C.c_int32),
         ("xcd_blocks", C.c_int32), ("scan_groups", C.c_int32), ("candidate_cache", C.c_int32),
         ("candidate_margin", C.c_int32), ("certify_prev", C.c_int32), ("query_order", C.c_int32),
         ("overflow_halves", C.c_int32), ("device_loop", C.c_int32), ("timing_stride", C.c_int32),
         ("candidate_loose", C.c_int32), ("candidate_lead", C.c_int32), ("fused_cull", C.c_int32),
-        ("peer_timeout_ms", C.c_int32), ("no_warmup", C.c_int32), ("ball_mode", C.c_int32), ("reserved", C.c_int32 * 4), ("config_version", C.c_uint32),
+        ("peer_timeout_ms", C.c_int32), ("no_warmup", C.c_int32), ("ball_mode", C.c_int32), ("reserved", C.c_int32 * 4),
     ]
 
 
@@ -368,8 +368,15 @@ class Context:
                 return 0
             except Exception:
                 return 1
-        self._xcb = _EXCHANGE_FN(_cb)  # kept alive as long as the context
-        _check(lib().icp_hip_comm_init_host(self._h, nranks, rank, C.cast(self._xcb, C.c_void_p), None))
+        new_cb = _EXCHANGE_FN(_cb)
+        # the previous callback may still run on the context's exchange thread (abandoned at the
+        # deadline) until icp_hip_comm_init_host joins it: its thunk stays alive for the whole
+        # call, and for the context's life (retired callbacks are kept until close)
+        if getattr(self, "_xcb", None) is not None:
+            self._xcb_retired = getattr(self, "_xcb_retired", []) + [self._xcb]
+        rc = lib().icp_hip_comm_init_host(self._h, nranks, rank, C.cast(new_cb, C.c_void_p), None)
+        self._xcb = new_cb  # kept alive as long as the context
+        _check(rc)
 
     def set_target(self, xyz, max_points=10, max_depth=20, rules=RULES_ENGINE):
         xyz = _aos(xyz)

@@ -199,8 +199,9 @@ int icp_source_shard_order(const double* xyz, int64_t n, int32_t* order) {
 }
 
 int icp_synth_pair(const icp_synth_spec* s, int64_t n_tgt, int64_t n_src, double* tgt, double* src, double T_true[16]) {
-  if (!s || n_tgt < 0 || n_src < 0 || n_src > n_tgt || (n_tgt > 0 && !tgt) || (n_src > 0 && !src)) {
-    icp_ctx_set_error("icp_synth_pair: bad arguments (need 0 <= n_src <= n_tgt)");
+  if (!s || n_tgt < 0 || n_src < 0 || n_src > n_tgt || (n_tgt > 0 && !tgt) || (n_src > 0 && !src) ||
+      !(s->outlier_fraction >= 0.0 && s->outlier_fraction <= 1.0)) {
+    icp_ctx_set_error("icp_synth_pair: bad arguments (need 0 <= n_src <= n_tgt, outlier_fraction in [0, 1])");
     return -1;
   }
   // R = Rz(yaw) Ry(pitch) Rx(roll) as test_icp.cpp:165-189
@@ -249,12 +250,14 @@ int icp_synth_pair(const icp_synth_spec* s, int64_t n_tgt, int64_t n_src, double
   }
   const uint64_t noise_seed = s->seed_source;
   const uint64_t outlier_seed = s->seed_source ^ 0x27d4eb2f165667c5ull;
-  const uint64_t thresh = (uint64_t)(s->outlier_fraction * 18446744073709551616.0);
+  // f in [0, 1); f = 1: every point (the cast of 2^64 would be undefined)
+  const bool all = s->outlier_fraction >= 1.0;
+  const uint64_t thresh = all ? 0 : (uint64_t)(s->outlier_fraction * 18446744073709551616.0);
 #pragma omp parallel for schedule(static)
   for (int64_t i = 0; i < n_src; i++) {
     double* o = src + 3 * i;
     const uint64_t pick = rng_at(outlier_seed, (uint64_t)(4 * i));
-    if (s->outlier_fraction > 0 && pick < thresh) {
+    if (s->outlier_fraction > 0 && (all || pick < thresh)) {
       for (int k = 0; k < 3; k++) o[k] = lo[k] + (hi[k] - lo[k]) * u01(rng_at(outlier_seed, (uint64_t)(4 * i + 1 + k)));
       continue;
     }
@@ -374,7 +377,8 @@ extern "C" {
 int icp_synth_scene(const icp_scene_spec* s, int64_t n_tgt, int64_t n_src, double* tgt, double* src,
                     double T_true[16]) {
   if (!s || n_tgt < 0 || n_src < 0 || (n_tgt > 0 && !tgt) || (n_src > 0 && !src) || !(s->site_radius > 0.0) ||
-      s->n_walls < 0 || s->n_walls > 4096 || !(s->elev_max_deg > s->elev_min_deg) || !(s->quantum >= 0.0)) {
+      s->n_walls < 0 || s->n_walls > 4096 || !(s->elev_max_deg > s->elev_min_deg) || !(s->quantum >= 0.0) ||
+      !(s->outlier_fraction >= 0.0 && s->outlier_fraction <= 1.0)) {
     icp_ctx_set_error("icp_synth_scene: bad arguments");
     return -1;
   }
@@ -417,10 +421,12 @@ int icp_synth_scene(const icp_scene_spec* s, int64_t n_tgt, int64_t n_src, doubl
     }
   }
   const uint64_t oseed = s->seed_source ^ 0x13198a2e03707344ull;
-  const uint64_t thresh = (uint64_t)(s->outlier_fraction * 18446744073709551616.0);
+  // f in [0, 1); f = 1: every point (the cast of 2^64 would be undefined)
+  const bool all = s->outlier_fraction >= 1.0;
+  const uint64_t thresh = all ? 0 : (uint64_t)(s->outlier_fraction * 18446744073709551616.0);
   if (s->outlier_fraction > 0)
     for (int64_t i = 0; i < n_src; i++)
-      if (rng_at(oseed, (uint64_t)(4 * i)) < thresh)
+      if (all || rng_at(oseed, (uint64_t)(4 * i)) < thresh)
         for (int k = 0; k < 3; k++)
           src[3 * i + k] = quantize(lo[k] + (hi[k] - lo[k]) * u01(rng_at(oseed, (uint64_t)(4 * i + 1 + k))), s->quantum);
   return 0;

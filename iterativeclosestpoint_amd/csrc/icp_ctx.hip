@@ -212,10 +212,14 @@ int icp_hip_create_ex(icp_hip_ctx** out, int device, const icp_hip_config* cfg) 
   *out = nullptr;
   icp_hip_config conf;
   icp_hip_config_default(&conf);
-  if (cfg) conf = *cfg;
-  if (conf.config_version != ICP_HIP_CONFIG_VERSION)
+  // the version word comes first: checked before the struct is copied (a struct of another
+  // header version may be shorter than this one)
+  if (cfg && cfg->config_version != ICP_HIP_CONFIG_VERSION)
     return fail(ICP_HIP_EINVAL, "config: config_version is not ICP_HIP_CONFIG_VERSION (start from icp_hip_config_default "
                                 "of this header)");
+  if (cfg) conf = *cfg;
+  for (int k = 0; k < 4; k++)
+    if (conf.reserved[k] != 0) return fail(ICP_HIP_EINVAL, "config: reserved words must be zero");
   if (conf.peer_timeout_ms < 0) return fail(ICP_HIP_EINVAL, "config: peer_timeout_ms must be >= 0");
   if (conf.no_warmup != 0 && conf.no_warmup != 1) return fail(ICP_HIP_EINVAL, "config: no_warmup must be 0 or 1");
   if (conf.ball_mode < 0 || conf.ball_mode > 2) return fail(ICP_HIP_EINVAL, "config: ball_mode out of [0, 2]");
@@ -643,18 +647,28 @@ int icp_hip_set_source(icp_hip_ctx* c, const double* xyz, int64_t n) {
 
 // The host's wait for the device (the only wait of an iterate or of a device-loop batch): `done`
 // polled in a tight loop; every 1024 polls the group's abort flag, the stream's own errors and,
-// with peers (an RCCL communicator or the host exchange), the communicator's asynchronous error
-// and config.peer_timeout_ms. A peer process that died or a broken link leaves this rank's
-// ncclAllGather waiting forever on the device: RCCL reports it as the communicator's async error,
-// and the deadline covers what it does not see. Either way the communicator is aborted (the
-// pending collective returns, the stream drains) and iterates fail with ERCCL until comm_init.
-template <class Done>
-static int wait_device(icp_hip_ctx* c, Done done, const char* what) {
+// over an RCCL communicator, the communicator's asynchronous error and config.peer_timeout_ms. A
+// peer process that died or a broken link leaves this rank's ncclAllGather waiting forever on the
+// device: RCCL reports it as the communicator's async error, and the deadline covers what it does
+// not see. Either way the communicator is aborted (the pending collective returns, the stream
+// drains) and iterates fail with ERCCL until comm_init. The deadline is per iterate: `progress`
+// (a count of the iterates the device has finished, e.g. a device-loop batch's published ring
+// records) restarts it, so a long batch of healthy iterates is not a stalled peer. (The host
+// exchange needs no deadline here: its callback ran, under its own deadline, before this wait,
+// which then covers device work only.)
+template <class Done, class Progress>
+static int wait_device(icp_hip_ctx* c, Done done, Progress progress, const char* what) {
   hipStream_t s = c->stream;
-  const bool peers = c->comm != nullptr || (c->xfn != nullptr && c->nranks > 1);
-  const auto t0 = std::chrono::steady_clock::now();
+  const bool peers = c->comm != nullptr;
+  auto t0 = std::chrono::steady_clock::now();
+  uint64_t seen = progress();
   for (unsigned spin = 1; !done(); spin++) {
     if ((spin & 1023u) != 0) continue;
+    const uint64_t now_p = progress();
+    if (now_p != seen) {  // the device finished an iterate: the deadline starts again
+      seen = now_p;
+      t0 = std::chrono::steady_clock::now();
+    }
     if (c->abort && c->abort->load()) return fail(ICP_HIP_EEXCHANGE, std::string(what) + ": a peer device of the group failed");
     if (c->comm) {
       ncclResult_t ae = ncclSuccess;
@@ -806,7 +820,9 @@ int icp_hip_iterate(icp_hip_ctx* c, const double* T_apply, int iter, int rules, 
     uint64_t want_bits;
     std::memcpy(&want_bits, &want, sizeof(want));
     const uint64_t* word = reinterpret_cast<const uint64_t*>(&c->h_it->pad[3]);
-    const int wrc = wait_device(c, [&]() { return __atomic_load_n(word, __ATOMIC_ACQUIRE) == want_bits; }, "iterate");
+    const int wrc = wait_device(
+        c, [&]() { return __atomic_load_n(word, __ATOMIC_ACQUIRE) == want_bits; }, []() { return (uint64_t)0; },
+        "iterate");
     if (wrc != ICP_HIP_OK) return wrc;
   }
   c->lists_zero = true;
@@ -856,6 +872,10 @@ int icp_hip_loop_run(icp_hip_ctx* c, icp::SessionCore* core, const icp::SessionP
   c->h_loop->p = *p;
   HIP_TRY(hipMemcpyAsync(c->loopd, c->h_loop, sizeof(LoopDev), hipMemcpyHostToDevice, s));
   HIP_TRY(hipEventRecord(c->ev_batch, s));
+  // the ring slots' outcome words, cleared to a sentinel: the batch's last kernels overwrite them
+  // one iterate at a time (the host wait's progress)
+  constexpr int32_t kUnset = 0x7fffffff;
+  for (int j = 0; j < k; j++) __atomic_store_n(&c->h_ring[j].outcome, kUnset, __ATOMIC_RELAXED);
   const int64_t first = c->n_iterates;
   // Iteration j > 0 runs only if iteration j - 1 left the session going, i.e. produced a
   // transform: its search applies it. The first applies the session's pending increment.
@@ -866,7 +886,14 @@ int icp_hip_loop_run(icp_hip_ctx* c, icp::SessionCore* core, const icp::SessionP
   HIP_TRY(hipMemcpyAsync(c->h_loop, c->loopd, sizeof(LoopDev), hipMemcpyDeviceToHost, s));
   // (polled rather than hipStreamSynchronize: a batch over a communicator whose peer died would
   // otherwise wait forever)
-  const int wrc = wait_device(c, [&]() { return hipStreamQuery(s) != hipErrorNotReady; }, "device loop");
+  const int wrc = wait_device(
+      c, [&]() { return hipStreamQuery(s) != hipErrorNotReady; },
+      [&]() {
+        uint64_t n = 0;
+        for (int j = 0; j < k; j++) n += __atomic_load_n(&c->h_ring[j].outcome, __ATOMIC_RELAXED) != kUnset ? 1u : 0u;
+        return n;
+      },
+      "device loop");
   if (wrc != ICP_HIP_OK) return wrc;
   const hipError_t e = hipStreamSynchronize(s);
   if (e != hipSuccess) return fail(ICP_HIP_EDEVICE, std::string("device loop: ") + hipGetErrorString(e));

@@ -114,6 +114,10 @@ extern "C" int icp_hip_create_multi(icp_hip_ctx** out, int n_devices, const int*
     if (n_devices == 1) return icp_hip_create_ex(out, devs[0], cfg);  // a plain single-device context
     transport = distinct ? ICP_XPORT_RCCL : ICP_XPORT_HOST;
   }
+  // the version word first, before the struct is copied (icp_hip_create_ex checks the rest)
+  if (cfg && cfg->config_version != ICP_HIP_CONFIG_VERSION)
+    return fail(ICP_HIP_EINVAL, "config: config_version is not ICP_HIP_CONFIG_VERSION (start from icp_hip_config_default "
+                                "of this header)");
   auto* g = new DeviceGroup();
   g->devices = devs;
   g->transport = transport;

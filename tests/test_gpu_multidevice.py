@@ -305,3 +305,24 @@ def test_rccl_deadline_aborts_and_recovers(icp):
         ctx.comm_init(1, 0, icp.Context.unique_id())
         st = ctx.iterate(None, 0, icp.RULES_ENGINE, 3.0)
         assert st.n == src.shape[0]
+
+
+def test_device_loop_batch_longer_than_deadline(icp):
+    """config.peer_timeout_ms bounds ONE iterate, not a device-loop batch: a batch of 80 healthy
+    iterates over an RCCL communicator that takes several times the deadline completes (the ring
+    records the device publishes restart the deadline)."""
+    import time
+    tgt, src, _ = icp.synth_pair(5_000_000)
+    with icp.Context(0, icp.config(peer_timeout_ms=8, device_loop=1)) as ctx:
+        ctx.set_target(tgt, 10, 20, icp.RULES_ENGINE)
+        ctx.set_source(src)
+        ctx.synchronize()
+        ctx.comm_init(1, 0, icp.Context.unique_id())
+        p = icp.params_default(max_iterations=100, tolerance=0.0, flags=icp.FLAG_NO_EARLY_STOP)
+        s = ctx.session(p)
+        assert s.step_n(2) == 2
+        t0 = time.perf_counter()
+        assert s.step_n(80) == 80
+        wall_ms = (time.perf_counter() - t0) * 1e3
+        assert wall_ms > 2 * 8, wall_ms  # the batch really outlasted the per-iterate deadline
+        s.close()

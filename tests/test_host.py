@@ -171,3 +171,20 @@ def test_source_shard_order_is_a_spatial_permutation(icp):
         vol_kd += np.prod(np.percentile(a, 95, 0) - np.percentile(a, 5, 0))
         vol_plain += np.prod(np.percentile(b, 95, 0) - np.percentile(b, 5, 0))
     assert vol_kd < 0.4 * vol_plain
+
+
+def test_synth_outlier_fraction_is_validated(icp):
+    """outlier_fraction outside [0, 1] (or NaN) is refused; 1.0 makes every source point an outlier
+    (no undefined float -> uint64 cast of 2^64)."""
+    for f in (-0.1, 1.5, float("nan")):
+        with pytest.raises(icp.IcpError):
+            icp.synth_pair(100, outlier_fraction=f)
+        with pytest.raises(icp.IcpError):
+            icp.synth_scene(100, outlier_fraction=f)
+    tgt, src, _ = icp.synth_pair(500, outlier_fraction=1.0, noise_sigma=0.0)
+    lo, hi = tgt.min(axis=0), tgt.max(axis=0)
+    assert np.all((src >= lo) & (src <= hi))
+    _, src0, _ = icp.synth_pair(500, outlier_fraction=0.0, noise_sigma=0.0)
+    assert not np.any(np.all(src == src0, axis=1))  # no point kept its inlier position
+    tgt_s, src_s, _ = icp.synth_scene(500, outlier_fraction=1.0)
+    assert np.isfinite(src_s).all()
