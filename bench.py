@@ -67,6 +67,7 @@ NODE_B = 56  # box (48 B) + topology (8 B) of a node record
 
 
 TIMING_STRIDE = 8
+PEER_TIMEOUT_MS = 10_000
 
 
 def search_source_sha1() -> str:
@@ -75,6 +76,13 @@ def search_source_sha1() -> str:
     for f in SEARCH_SOURCES:
         h.update((ROOT / "iterativeclosestpoint_amd" / "csrc" / f).read_bytes())
     return h.hexdigest()
+
+
+def workload_key(args) -> str:
+    """The data a PMC profile was taken on (tools/profile_bench.sh WORKLOAD): counters of one
+    workload never describe another's kernel."""
+    return f"{'scene' if args.scene else 'blob'}|q={float(args.quantize)}|dup={int(args.duplicates)}" + (
+        "" if args.scene_outliers is None else f"|out={float(args.scene_outliers)}")
 
 
 def shard_range(n: int, rank: int, world: int) -> tuple[int, int]:
@@ -332,6 +340,10 @@ def main() -> int:
     # the search kernel is timed (HIP events on its dispatch and the next kernel's) on every 8th
     # iterate: an event on a dispatch packet delays the next kernel by ~3-5 us (25 samples of 200)
     kv = {"timing_stride": str(TIMING_STRIDE)}
+    if shards > 1:
+        # a stalled or dead peer ends the run with ICP_HIP_ERCCL instead of a hang (per iterate;
+        # the first iterate of a 10M scene shard takes ~0.1 s)
+        kv["peer_timeout_ms"] = str(PEER_TIMEOUT_MS)
     kv.update(dict(c.split("=", 1) for c in args.config))
     conf = icp.config(**{k: (float(v) if "." in v else int(v)) for k, v in kv.items()})
     ctx = icp.Context(devices=[k % n_dev for k in range(args.gpus)], cfg=conf) if group else icp.Context(device, conf)
@@ -398,6 +410,27 @@ def main() -> int:
         elapsed, med_ms = float(t[0].item()), float(t[1].item())
     # HIP events of the timed iterates (read after the timed region)
     nn_ms, it_ms = ctx.timings(min(args.steps, 256))
+    comm = None
+    if shards > 1 or args.rccl_self:
+        # what RCCL itself reports (ncclCommCount / ncclCommUserRank / ncclCommCuDevice) for every
+        # rank, and each rank's exchange time (events around the two all-gathers, timed iterates)
+        xms = ctx.exchange_timings(min(args.steps, 256))
+        xms = xms[np.isfinite(xms)]
+        mine = [dict(ctx.comm_info(m), hip_device=dev, pid=os.getpid(),
+                     exchange_ms_mean=None if len(xms) == 0 else round(float(np.mean(xms)), 4),
+                     exchange_ms_max=None if len(xms) == 0 else round(float(np.max(xms)), 4),
+                     exchange_samples=int(len(xms)))
+                for m, dev in ((k, d) for k, d in enumerate(ctx.devices()[0] if group else [device]))]
+        if world > 1:
+            allr = [None] * world
+            dist.all_gather_object(allr, mine)
+            mine = [r for per in allr for r in per]
+        comm = {"ranks": mine, "rccl_count_ok": all(r["count"] == shards for r in mine),
+                "rank_set_ok": sorted(r["rank"] for r in mine) == list(range(shards)),
+                "peer_timeout_ms": int(conf.peer_timeout_ms),
+                "note": "count/rank/device: RCCL's own view (icp_hip_comm_info); exchange_ms: the two per-iteration "
+                        "record all-gathers (HIP events on the compute stream, includes waiting for the slowest "
+                        "peer; host clock for the host exchange), timed iterates (every 8th) of the timed region"}
     # untimed: the state the last timed iterate left (its queries = the moved source, and its
     # correspondences/residuals), checked against the CPU oracle below
     timed_q = timed_idx = timed_d = None
@@ -422,8 +455,10 @@ def main() -> int:
     if tj.exists():
         try:
             tr = json.loads(tj.read_text())
-            # only a profile of this exact kernel source and workload counts
-            if tr.get("n") == n and tr.get("world") == shards and tr.get("search_src_sha1") == search_source_sha1():
+            # only a profile of this exact kernel source and workload counts (a profile written before
+            # the workload key existed is of config 4's blob)
+            if (tr.get("n") == n and tr.get("world") == shards and tr.get("search_src_sha1") == search_source_sha1()
+                    and tr.get("workload", "blob|q=0.0|dup=1") == workload_key(args)):
                 traffic = tr.get("bytes_per_launch")
                 if tr.get("valu_issue_frac") is not None:
                     # the bound that binds the search kernel: VALU issue (SQ counters of the same
@@ -544,6 +579,7 @@ def main() -> int:
                       "note": "host synthesis; set_target = upload + device octree build + tables; "
                               "set_source = query order + upload (+ communicator setup for N > 1)"},
             "octree_build": {"on_device": build_on_dev, "ms": round(build_ms, 2)},
+            "comm": comm,
             "final_rmse": res.final_rmse,
         }
         print(json.dumps(line), flush=True)

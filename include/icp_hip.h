@@ -155,7 +155,14 @@ typedef struct icp_hip_config {
                               queries per wave (16-lane ball walks, follow-ups for the balls that
                               overflow); 1 always the ball walk; 2 always whole queries. The same
                               results either way                          dflt 0 */
-  int32_t reserved[4];     /* zero (fields of later versions of this header); create_ex rejects
+  int32_t wide_pass;       /* the wave search's boxes that hold more candidates than its LDS list
+                              (a box 10-100x denser than its queries: surface data far from
+                              convergence, occlusion shadows): 0 (auto) searched again by the wide
+                              pass (k_nn_wide: the same box walked and scanned in segments by the
+                              same 64 lanes) in a source's first iterate and whenever the previous
+                              iterate had >= 256 such waves, else their queries take the ball
+                              search; 1 never; 2 always. The same results either way     dflt 0 */
+  int32_t reserved[3];     /* zero (fields of later versions of this header); create_ex rejects
                               a nonzero word                                                    */
 } icp_hip_config;
 #define ICP_HIP_CONFIG_VERSION 3u /* 1: r4 and earlier (no version field); 2: r5 (version last) */
@@ -192,8 +199,6 @@ typedef struct icp_hip_config {
 #define ICP_DBG_START_NODES 21   /* start nodes taken from the cell tables / descent levels    */
 #define ICP_DBG_WINNER_PREV 22   /* winner-count build: joined lanes whose winner is the previous match */
 #define ICP_DBG_WINNER_LANES 23  /* winner-count build: joined lanes with an fp32 winner          */
-#define ICP_DBG_BB_OVERFLOW 23   /* other builds: cooperative searches whose frontier still
-                                    overflowed after their restarts (the reference-order DFS ran) */
 #define ICP_DBG_WALK_MOVED 24   /* waves with a record of this generation that walked because
                                     their box left B+                                        */
 #define ICP_DBG_WALK_LOOSE 25   /* waves whose box lay inside B+ but walked because B+ was loose */
@@ -204,7 +209,15 @@ typedef struct icp_hip_config {
 #define ICP_DBG_FZ_RECOMPUTE 30 /* waves whose covariance record the cull recomputes (queries
                                    left to the other searches)                                 */
 #define ICP_DBG_FZ_BAND 31      /* queries in the band around the previous threshold           */
-#define ICP_DBG_SLOTS 32
+#define ICP_DBG_WIDE_WAVES 32    /* waves (or halves) the wide pass searched again               */
+#define ICP_DBG_WIDE_SEGMENTS 33 /* candidate-list segments the wide pass scanned                 */
+#define ICP_DBG_WIDE_STACK 34    /* wide walks whose node stack overflowed (lanes to the ball search) */
+#define ICP_DBG_WIDE_UNDECIDED 35 /* lanes the wide pass left to the ball search (no certificate) */
+#define ICP_DBG_WIDE_POINTS 36   /* candidate points listed by the wide walks                      */
+#define ICP_DBG_BB_OVERFLOW 37   /* cooperative searches whose frontier still outgrew the stack  */
+#define ICP_DBG_LANE_EXACT 38    /* queries the ball search finished by the reference-order DFS
+                                    after the cooperative search (a tie or an overflow)          */
+#define ICP_DBG_SLOTS 40
 
 typedef struct icp_hip_ctx icp_hip_ctx;
 
@@ -305,6 +318,22 @@ int icp_hip_comm_init_host(icp_hip_ctx* ctx, int nranks, int rank, icp_hip_excha
  * keeps running on the context's exchange thread and must return eventually: comm_init,
  * comm_init_host and icp_hip_destroy wait for it. */
 int icp_hip_comm_abort(icp_hip_ctx* ctx);
+
+/* The communicator as RCCL itself reports it (ncclCommCount, ncclCommUserRank, ncclCommCuDevice)
+ * for member `member` of a context (0 for a single-device context; a device group's members in
+ * device-list order), and its transport (ICP_XPORT_RCCL, ICP_XPORT_CALLBACK for the host
+ * exchange, ICP_XPORT_AUTO for none). Without an RCCL communicator: the context's own world size,
+ * rank and device. Lets a launcher check that RCCL saw the world it asked for. Any output may be
+ * null. Replaces nothing in the reference (single-process CPU code). */
+int icp_hip_comm_info(icp_hip_ctx* ctx, int member, int32_t* count, int32_t* rank, int32_t* device,
+                      int32_t* transport);
+
+/* Time (ms) of the two per-iteration record all-gathers of each of the last k iterates (k <= 256),
+ * oldest first: HIP events around the RCCL all-gathers on the compute stream (so the figure
+ * includes waiting for the slowest peer to arrive), or the host clock around the host exchange's
+ * callback. NaN for an iterate that config.timing_stride left untimed or that ran without peers.
+ * A device group reports its slowest member per iterate. Waits for the iterates to finish. */
+int icp_hip_exchange_timings(icp_hip_ctx* ctx, int k, double* exchange_ms);
 
 /* Build the reference octree of the target (AoS xyz, n points) and keep it in HBM. The tree is
  * built on the device (max_depth <= 21, config octree_builder AUTO) or on the host (deeper

@@ -25,16 +25,17 @@ XPORT_HOST = 2
 XPORT_CALLBACK = 3
 # icp_hip.h error codes (IcpError.code)
 OK, EINVAL, ENOMEM, EDEVICE, ERCCL, ENOTREADY, EEXCHANGE = 0, -1, -2, -3, -4, -5, -6
-DBG_SLOTS = 32
+DBG_SLOTS = 40
 # icp_hip.h ICP_DBG_* slot names
 DBG_NAMES = {0: "waves", 1: "overflow_waves", 2: "not_joined", 3: "not_covered", 4: "scanned_points",
              8: "fp64_scan_waves", 9: "staged_points", 10: "scan_pairs", 11: "scan_rounds",
              12: "cache_hits", 13: "cache_stores",
              5: "walk_batches", 6: "no_guess", 7: "candidates", 14: "ball_overflow", 15: "ball_points",
-             21: "start_nodes", 20: "winner_prev_waves", 22: "winner_prev", 23: "bb_overflow",
+             21: "start_nodes", 20: "winner_prev_waves", 22: "winner_prev", 23: "winner_lanes",
              18: "prev_cert_waves", 19: "prev_cert_lanes", 16: "halves", 17: "reused_entries",
              24: "walk_moved", 25: "walk_loose", 26: "group_points", 27: "bb_queries", 28: "bb_steps",
-             29: "lane_handed", 30: "fz_recompute", 31: "fz_band"}
+             29: "lane_handed", 30: "fz_recompute", 31: "fz_band", 32: "wide_waves", 33: "wide_segments",
+             34: "wide_stack", 35: "wide_undecided", 36: "wide_points", 37: "bb_overflow", 38: "lane_exact"}
 
 _P = C.c_void_p
 _D = C.POINTER(C.c_double)
@@ -73,7 +74,7 @@ class HipConfig(C.Structure):
         ("candidate_margin", C.c_int32), ("certify_prev", C.c_int32), ("query_order", C.c_int32),
         ("overflow_halves", C.c_int32), ("device_loop", C.c_int32), ("timing_stride", C.c_int32),
         ("candidate_loose", C.c_int32), ("candidate_lead", C.c_int32), ("fused_cull", C.c_int32),
-        ("peer_timeout_ms", C.c_int32), ("no_warmup", C.c_int32), ("ball_mode", C.c_int32), ("reserved", C.c_int32 * 4),
+        ("peer_timeout_ms", C.c_int32), ("no_warmup", C.c_int32), ("ball_mode", C.c_int32), ("wide_pass", C.c_int32), ("reserved", C.c_int32 * 3),
     ]
 
 
@@ -175,6 +176,8 @@ SIGNATURES = {
     "icp_hip_last_timing": (C.c_int, [_P, _D, _D]),
     "icp_hip_last_cull_path": (C.c_int, [_P, _I32]),
     "icp_hip_timings": (C.c_int, [_P, C.c_int, _P, _P]),
+    "icp_hip_exchange_timings": (C.c_int, [_P, C.c_int, _P]),
+    "icp_hip_comm_info": (C.c_int, [_P, C.c_int, _I32, _I32, _I32, _I32]),
     "icp_hip_target_build_info": (C.c_int, [_P, _I32, _D]),
     "icp_hip_copy_target": (C.c_int, [_P, _P, _P, _P, _P, _P, _P]),
     "icp_hip_target_separation": (C.c_int, [_P, _P]),
@@ -472,6 +475,18 @@ class Context:
         a, b = np.zeros(k), np.zeros(k)
         _check(lib().icp_hip_timings(self._h, k, _ptr(a), _ptr(b)))
         return a, b
+
+    def exchange_timings(self, k: int):
+        """ms of the two record all-gathers of each of the last k iterates (NaN: not timed)."""
+        a = np.zeros(k)
+        _check(lib().icp_hip_exchange_timings(self._h, k, _ptr(a)))
+        return a
+
+    def comm_info(self, member: int = 0) -> dict:
+        """The communicator of member `member` as RCCL reports it (icp_hip_comm_info)."""
+        n, r, d, t = C.c_int32(), C.c_int32(), C.c_int32(), C.c_int32()
+        _check(lib().icp_hip_comm_info(self._h, member, C.byref(n), C.byref(r), C.byref(d), C.byref(t)))
+        return {"count": n.value, "rank": r.value, "device": d.value, "transport": t.value}
 
     def synchronize(self):
         _check(lib().icp_hip_synchronize(self._h))

@@ -39,8 +39,18 @@ struct alignas(32) TgtPt {
   double x, y, z;
   int32_t orig;  // original index into the caller's target array
   float sep;     // lower bound of the exact distance from this point to every other target point
-                 // (0 = none known; computed on the device after either build, k_target_sep)
+                 // (0 = none known; computed on the device after either build, k_target_sep);
+                 // its sign bit: this point is a copy of an earlier one (k_mark_copies)
 };
+// Points a target point is compared with, looking back in leaf order, for its copy flag: a leaf
+// holds at most max_points (default 10) points unless it sits at the maximum depth.
+constexpr int kCopyWindow = 32;
+// The copy flag from the 64-bit word (orig, sep) of a point: sep's sign bit is the word's.
+ICP_HD bool tgt_copy_word(double w) {
+  long long b;
+  __builtin_memcpy(&b, &w, 8);
+  return b < 0;
+}
 static_assert(sizeof(TgtPt) == 32, "TgtPt must be 32 bytes");
 
 // Residual moments of one block / rank: count, mean, centered M2 (Chan et al. merge),

@@ -148,7 +148,8 @@ static void warm_kernels(int device, const icp_hip_config& conf) {
   const uint64_t key = (uint64_t)conf.search | (uint64_t)conf.scan_groups << 4 | (uint64_t)conf.certify_prev << 8 |
                        (uint64_t)(conf.debug_counters != 0) << 12 | (uint64_t)conf.fused_cull << 13 |
                        (uint64_t)conf.overflow_halves << 14 | (uint64_t)conf.scan32 << 15 |
-                       (uint64_t)conf.candidate_cache << 16 | (uint64_t)conf.ball_mode << 17;
+                       (uint64_t)conf.candidate_cache << 16 | (uint64_t)conf.ball_mode << 17 |
+                       (uint64_t)conf.wide_pass << 19;
   std::lock_guard<std::mutex> lk(mu);
   for (const auto& d : done)
     if (d.first == device && d.second == key) return;
@@ -218,8 +219,9 @@ int icp_hip_create_ex(icp_hip_ctx** out, int device, const icp_hip_config* cfg) 
     return fail(ICP_HIP_EINVAL, "config: config_version is not ICP_HIP_CONFIG_VERSION (start from icp_hip_config_default "
                                 "of this header)");
   if (cfg) conf = *cfg;
-  for (int k = 0; k < 4; k++)
+  for (int k = 0; k < 3; k++)
     if (conf.reserved[k] != 0) return fail(ICP_HIP_EINVAL, "config: reserved words must be zero");
+  if (conf.wide_pass < 0 || conf.wide_pass > 2) return fail(ICP_HIP_EINVAL, "config: wide_pass out of [0, 2]");
   if (conf.peer_timeout_ms < 0) return fail(ICP_HIP_EINVAL, "config: peer_timeout_ms must be >= 0");
   if (conf.no_warmup != 0 && conf.no_warmup != 1) return fail(ICP_HIP_EINVAL, "config: no_warmup must be 0 or 1");
   if (conf.ball_mode < 0 || conf.ball_mode > 2) return fail(ICP_HIP_EINVAL, "config: ball_mode out of [0, 2]");
@@ -317,6 +319,9 @@ void icp_hip_destroy(icp_hip_ctx* c) {
   for (hipEvent_t ev : {c->ev_it0, c->ev_it1})
     if (ev) (void)hipEventDestroy(ev);
   for (auto& r : c->ring)
+    for (hipEvent_t ev : r)
+      if (ev) (void)hipEventDestroy(ev);
+  for (auto& r : c->xring)
     for (hipEvent_t ev : r)
       if (ev) (void)hipEventDestroy(ev);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -490,6 +495,8 @@ int icp_hip_set_target(icp_hip_ctx* c, const double* xyz, int64_t n, int max_poi
   }
   // separation of every target point (the previous-match certificate, certify_prev)
   if (c->cfg.certify_prev) HIP_TRY(launch_target_sep(c->nodes, c->pts, n, c->levels, c->stream));
+  // after the separations (which a copy's flag overwrites: its separation is 0 either way)
+  HIP_TRY(launch_mark_copies(c->pts, n, c->stream));
   // root box (host copy: the kernels' cell arithmetic starts from it) and the cell tables
   {
     NodeRec root;
@@ -694,6 +701,20 @@ static int wait_device(icp_hip_ctx* c, Done done, Progress progress, const char*
   return ICP_HIP_OK;
 }
 
+// The wide pass's list: after the exact and ball lists (2 n ints) and the half list (<= 2 halves
+// of every wave, two ints each: <= n / 16 + 4 ints); <= 3 entries per wave (the wave and its two
+// halves), three ints each: inside the 3 n + 64 ints of fb_list.
+static int32_t* wide_list(int32_t* fbl, int64_t n) { return fbl + 2 * n + n / 16 + 8; }
+
+// config.wide_pass: 0 a source's first iterate (descent guesses: loose boxes) and any iterate after
+// one with >= kWideAuto overflowing waves (surface data far from convergence, occlusion shadows;
+// the ball search takes the queries of a few hundred waves sooner than a second launch); 2 always
+static constexpr double kWideAuto = 256.0;
+static bool wide_pass_on(const icp_hip_ctx* c) {
+  if (!c->cfg.scan32 || c->cfg.search != ICP_SEARCH_CERTIFIED || c->cfg.wide_pass == 1) return false;
+  return c->cfg.wide_pass == 2 || !c->have_prev || c->last_wide >= kWideAuto;
+}
+
 // One iterate enqueued on the context's stream, no wait. Host-driven (loop_slot < 0): the
 // transform T_apply (null: none) is a kernel argument and the last kernel publishes the record
 // with sequence number *seq for the host's poll. Device loop (loop_slot >= 0): the transform is
@@ -723,6 +744,7 @@ static int enqueue_iterate(icp_hip_ctx* c, const double* T_apply, bool apply, in
   // guesses, loose boxes; ~16 % of the waves at 10M). Later iterates overflow in ~0.2 % of the
   // waves, whose queries the ball search finishes sooner than a second serial launch.
   a.fb_list3 = (c->cfg.overflow_halves && !c->have_prev) ? c->fb_list + 2 * c->n_src : nullptr;  // <= n + 64 ints
+  a.fb_list4 = wide_pass_on(c) ? wide_list(c->fb_list, c->n_src) : nullptr;
   a.fb_u2 = c->fb_u;
   a.fb_count = c->fb_count;
   a.have_prev = c->have_prev ? 1 : 0;
@@ -765,9 +787,26 @@ static int enqueue_iterate(icp_hip_ctx* c, const double* T_apply, bool apply, in
   cl.dist = c->dist;
   cl.wstat = a.wstat;
   HIP_TRY(launch_moments_tail(c->dist, c->n_src, c->mparts, loop, c->tickets, c->it, multi ? nullptr : &fin, cl, s));
+  // a timed multi-rank iterate also times its two record exchanges (icp_hip_exchange_timings):
+  // events around the all-gathers over RCCL, the host clock around the host exchange's callback
+  c->xtimed[slot] = (int8_t)(timed && multi ? (c->comm ? 1 : 2) : 0);
+  c->xhost_ms[slot] = 0.0;
+  hipEvent_t* xev = c->xring[slot];
+  if (c->xtimed[slot] == 1)
+    for (int k = 0; k < 4; k++)
+      if (!xev[k]) HIP_TRY(hipEventCreateWithFlags(&xev[k], hipEventDisableSystemFence));
+  auto gather_timed = [&](int which, const double* d_local, double* d_gathered, int count) {
+    if (c->xtimed[slot] == 1) HIP_TRY(hipEventRecord(xev[2 * which], s));
+    const auto h0 = std::chrono::steady_clock::now();
+    const int rc = all_gather_record(c, d_local, d_gathered, count, s);
+    if (c->xtimed[slot] == 2)
+      c->xhost_ms[slot] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h0).count();
+    if (rc == ICP_HIP_OK && c->xtimed[slot] == 1) HIP_TRY(hipEventRecord(xev[2 * which + 1], s));
+    return rc;
+  };
   if (multi) {
-    const int rc = all_gather_record(c, reinterpret_cast<const double*>(&c->it->m_local),
-                                     reinterpret_cast<double*>(c->gm), (int)(sizeof(Moments) / sizeof(double)), s);
+    const int rc = gather_timed(0, reinterpret_cast<const double*>(&c->it->m_local), reinterpret_cast<double*>(c->gm),
+                                (int)(sizeof(Moments) / sizeof(double)));
     if (rc != ICP_HIP_OK) return rc;
     HIP_TRY(launch_finalize_moments(c->gm, c->nranks, c->it, fin, cl, s));
   }
@@ -786,8 +825,8 @@ static int enqueue_iterate(icp_hip_ctx* c, const double* T_apply, bool apply, in
   }
   HIP_TRY(launch_cull_tail(cl, c->tickets + ticket_words() / 2, multi ? nullptr : &pub, s));
   if (multi) {
-    const int rc = all_gather_record(c, reinterpret_cast<const double*>(&c->it->c_local),
-                                     reinterpret_cast<double*>(c->gc), (int)(sizeof(CovMoments) / sizeof(double)), s);
+    const int rc = gather_timed(1, reinterpret_cast<const double*>(&c->it->c_local), reinterpret_cast<double*>(c->gc),
+                                (int)(sizeof(CovMoments) / sizeof(double)));
     if (rc != ICP_HIP_OK) return rc;
     HIP_TRY(launch_finalize_cov(c->gc, c->nranks, c->it, pub, s));
   }
@@ -828,6 +867,7 @@ int icp_hip_iterate(icp_hip_ctx* c, const double* T_apply, int iter, int rules, 
   c->lists_zero = true;
   for (int k = 0; k < 3; k++) c->last_lists[k] = (unsigned int)c->h_it->pad[k];
   const IterDev& h = *c->h_it;
+  c->last_wide = h.n_wide;
   c->last_cull_path = h.cull_mode != 0.0 ? 1 : 0;
   out->n = (int64_t)h.m_global.n;
   out->mean = h.mean;
@@ -904,6 +944,7 @@ int icp_hip_loop_run(icp_hip_ctx* c, icp::SessionCore* core, const icp::SessionP
   for (int j = k - 1; j >= 0; j--)
     if (recs[j].outcome != icp::kStepNone) {
       for (int q = 0; q < 3; q++) c->last_lists[q] = (unsigned int)recs[j].lists[q];
+      c->last_wide = (double)recs[j].pad[0];
       break;
     }
   if (step_ms) {
@@ -1020,6 +1061,7 @@ int icp_hip_nn(icp_hip_ctx* c, const double* q, int64_t n, int32_t* idx_out, dou
     a.fb_list = fbl;
     a.fb_list2 = fbl + n;
     a.fb_list3 = c->cfg.overflow_halves ? fbl + 2 * n : nullptr;
+    a.fb_list4 = c->cfg.scan32 && c->cfg.wide_pass != 1 ? wide_list(fbl, n) : nullptr;
     a.fb_u2 = fbu;
     a.fb_count = c->fb_count;
     unsigned int lists4[4] = {0, 0, 0, 0};
@@ -1109,6 +1151,46 @@ int icp_hip_last_timing(icp_hip_ctx* c, double* nn_ms, double* it_ms) {
   if (!c->timed[(c->n_iterates - 1) % icp_hip_ctx::kTimingRing])
     return fail(ICP_HIP_ENOTREADY, "the last iterate was not timed (config.timing_stride)");
   return icp_hip_timings(c, 1, nn_ms, it_ms);
+}
+
+int icp_hip_exchange_timings(icp_hip_ctx* c, int k, double* ms) {
+  if (!c || k < 0 || (k > 0 && !ms)) return fail(ICP_HIP_EINVAL, "bad arguments");
+  if (c->group) return group_exchange_timings(c, k, ms);
+  if (k > icp_hip_ctx::kTimingRing || k > c->n_iterates) return fail(ICP_HIP_EINVAL, "fewer iterates recorded than asked");
+  HIP_TRY(hipSetDevice(c->device));
+  for (int j = 0; j < k; j++) {
+    const int64_t slot = (c->n_iterates - k + j) % icp_hip_ctx::kTimingRing;
+    HIP_TRY(hipEventSynchronize(c->ring[slot][2]));
+    double v = std::nan("");
+    if (c->xtimed[slot] == 1) {
+      float f0 = 0.f, f1 = 0.f;
+      HIP_TRY(hipEventElapsedTime(&f0, c->xring[slot][0], c->xring[slot][1]));
+      HIP_TRY(hipEventElapsedTime(&f1, c->xring[slot][2], c->xring[slot][3]));
+      v = (double)f0 + (double)f1;
+    } else if (c->xtimed[slot] == 2) {
+      v = c->xhost_ms[slot];
+    }
+    ms[j] = v;
+  }
+  return ICP_HIP_OK;
+}
+
+int icp_hip_comm_info(icp_hip_ctx* c, int member, int32_t* count, int32_t* rank, int32_t* device, int32_t* transport) {
+  if (!c) return fail(ICP_HIP_EINVAL, "null ctx");
+  if (c->group) return group_comm_info(c, member, count, rank, device, transport);
+  if (member != 0) return fail(ICP_HIP_EINVAL, "a single-device context has member 0 only");
+  int n = c->nranks, r = c->rank, d = c->device;
+  if (c->comm) {
+    // RCCL's own view of the communicator, not the arguments it was created with
+    RCCL_TRY(ncclCommCount(c->comm, &n));
+    RCCL_TRY(ncclCommUserRank(c->comm, &r));
+    RCCL_TRY(ncclCommCuDevice(c->comm, &d));
+  }
+  if (count) *count = n;
+  if (rank) *rank = r;
+  if (device) *device = d;
+  if (transport) *transport = c->comm ? ICP_XPORT_RCCL : c->xfn ? ICP_XPORT_CALLBACK : ICP_XPORT_AUTO;
+  return ICP_HIP_OK;
 }
 
 int icp_hip_last_cull_path(icp_hip_ctx* c, int32_t* fused) {

@@ -82,6 +82,11 @@ struct icp_hip_ctx {
   static constexpr int kTimingRing = 256;
   hipEvent_t ring[kTimingRing][3] = {};
   bool timed[kTimingRing] = {};  // the slot's search carries events (config.timing_stride)
+  // the record exchange of a timed multi-rank iterate: events before / after each of the two
+  // all-gathers (RCCL; created at first use), or the host clock around them (host exchange)
+  hipEvent_t xring[kTimingRing][4] = {};
+  int8_t xtimed[kTimingRing] = {};  // 0 not timed, 1 events (RCCL), 2 host clock
+  double xhost_ms[kTimingRing] = {};
   int64_t n_iterates = 0;
 
   // target (replicated on every rank)
@@ -113,6 +118,7 @@ struct icp_hip_ctx {
                                     // (zero between launches: the last block resets its own)
   unsigned long long* dbg = nullptr;
   unsigned int last_lists[3] = {0, 0, 0};  // exact / ball / per-lane list sizes of the last search
+  double last_wide = 0.0;  // waves whose candidate set overflowed in the last published iterate
   icp::Moments* mparts = nullptr;
   icp::CovMoments* cparts = nullptr;
   icp::WaveStat* wstat = nullptr;  // the search's per-wave covariance records (wave_stats.h)
@@ -190,6 +196,8 @@ int group_traversal_counts(icp_hip_ctx* c, double* mean_entries, double* mean_po
 int group_cull_path(icp_hip_ctx* c, int32_t* fused);
 int group_timings(icp_hip_ctx* c, int k, double* nn_ms, double* it_ms);
 int group_debug_counters(icp_hip_ctx* c, uint64_t out[ICP_DBG_SLOTS]);
+int group_exchange_timings(icp_hip_ctx* c, int k, double* ms);
+int group_comm_info(icp_hip_ctx* c, int member, int32_t* count, int32_t* rank, int32_t* device, int32_t* transport);
 int group_synchronize(icp_hip_ctx* c);
 int group_inject_failure(icp_hip_ctx* c, int member, int where);
 icp_hip_ctx* group_member(icp_hip_ctx* c, int k);

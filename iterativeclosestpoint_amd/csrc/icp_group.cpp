@@ -343,6 +343,25 @@ int group_timings(icp_hip_ctx* c, int k, double* nn_ms, double* it_ms) {
   return ICP_HIP_OK;
 }
 
+int group_exchange_timings(icp_hip_ctx* c, int k, double* ms) {
+  // per iterate, the slowest member's exchange (NaN when the iterate was not timed)
+  std::vector<double> a((size_t)k);
+  bool first = true;
+  for (icp_hip_ctx* m : c->group->members) {
+    const int rc = icp_hip_exchange_timings(m, k, a.data());
+    if (rc != ICP_HIP_OK) return rc;
+    for (int j = 0; j < k; j++) ms[j] = first || a[j] > ms[j] ? a[j] : ms[j];
+    first = false;
+  }
+  return ICP_HIP_OK;
+}
+
+int group_comm_info(icp_hip_ctx* c, int member, int32_t* count, int32_t* rank, int32_t* device, int32_t* transport) {
+  DeviceGroup* g = c->group;
+  if (member < 0 || member >= (int)g->members.size()) return fail(ICP_HIP_EINVAL, "comm_info: no such member");
+  return icp_hip_comm_info(g->members[member], 0, count, rank, device, transport);
+}
+
 int group_cull_path(icp_hip_ctx* c, int32_t* fused) {
   // 1 only when every member's cull took its search's wave records
   int32_t all = 1;

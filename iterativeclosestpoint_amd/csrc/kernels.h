@@ -36,7 +36,7 @@ struct IterDev {
   double fz_lo, fz_hi, fz_thr, fz_ok;
   double fz_sh[6];
   double cull_mode;  // this iterate: 1 = the search's wave records + the band pairs, 0 = full cull
-  double fz_pad;
+  double n_wide;     // this iterate: waves of the wave search whose candidate set overflowed
   double pad[4];
 };
 
@@ -94,10 +94,12 @@ struct NNLaunch {
   int32_t* fb_list2;        // queries a wave did not take -> ball search
   double* fb_u2;            // the distance guess u of each fb_list2 entry
   unsigned int* fb_count;   // [0] exact list, [1] ball list sizes; [2] per-lane searches, [3] DFS
-                            // finishes of the ball search (counts); [4] half list size; zero at
-                            // the launch
+                            // finishes of the ball search (counts); [4] half list size; [5] wide
+                            // list size; [6] overflowed waves of the wave search; zero at the launch
   int32_t* fb_list3;        // 32-query halves of overflowed waves, (half id, lane mask) pairs
                             // (null: no half pass)
+  int32_t* fb_list4;        // the wide pass (k_nn_wide): overflowed waves / halves as (first query,
+                            // lane mask low, high) triples; null: overflowed lanes take the ball search
   hipEvent_t ev_start;      // optional: the main search kernel's start and end, recorded by its
   hipEvent_t ev_fast_done;  // own dispatch (hipExtLaunchKernel: no marker packets between kernels)
   int have_prev;            // dist_out holds the previous residuals of these queries
@@ -127,6 +129,7 @@ int nn_block_threads(int levels);
 hipError_t launch_nn(const NNLaunch& a, hipStream_t s);
 // TgtPt::sep of every target point (lower bound of its distance to every other point).
 hipError_t launch_target_sep(const NodeRec* nodes, TgtPt* pts, int64_t n, int levels, hipStream_t s);
+hipError_t launch_mark_copies(TgtPt* pts, int64_t n, hipStream_t s);
 
 struct CullLaunch {
   const LoopDev* loop;  // device loop: nothing to do once the session is done

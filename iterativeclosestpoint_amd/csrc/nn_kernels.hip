@@ -106,6 +106,11 @@ constexpr int kWaveStartK = 2;   // start cells per lane (up to 128 start nodes 
 constexpr int kWavePoints = 1024;  // candidate list area (up to kWaveCandCap ids)
 static_assert(kWaveCandCap <= kWavePoints, "candidate list");
 constexpr int kWaveLds = kWaveQueue * 4 + kWavePoints * 4;  // 5 KB per wave
+constexpr int kWideQueue = 512;  // the wide pass's node stack (after its staging area)
+#ifndef ICP_WIDE_SEGS
+#define ICP_WIDE_SEGS 6
+#endif
+constexpr int kWideSegs = ICP_WIDE_SEGS;  // segments a wide walk scans before it gives up
 static_assert(kWaveQueue * 4 >= 64 * 16 && kWaveQueue * 4 >= 32 * 32, "staging area aliases the stack");
 static_assert(kWaveQueue * 4 + kWavePoints * 4 >= 128 * 16, "a reusing wave stages 128 points (stack + list area)");
 
@@ -162,6 +167,16 @@ __device__ __forceinline__ bool prev_certified(double u, float sep, double init_
   const double g = ((double)sep - dstar) * (1.0 - 0x1p-52);
   if (!(g > 0.0)) return false;
   return certified(u, g * g * (1.0 - 0x1p-50), init_best);
+}
+
+// A candidate point for the scans: x, y, z and its id (-1: a copy of an earlier point, whose twin
+// is the reference's answer whenever it would be; TgtPt::sep's sign, k_mark_copies). One 16-B load
+// of (x, y) and one of (z, orig | sep): the flag rides with z.
+__device__ __forceinline__ double4 load_cand(const TgtPt* pts, int32_t g) {
+  const TgtPt* p = pts + g;
+  const double2 xy = *reinterpret_cast<const double2*>(&p->x);
+  const double2 zw = *reinterpret_cast<const double2*>(&p->z);
+  return make_double4(xy.x, xy.y, zw.x, __longlong_as_double(tgt_copy_word(zw.y) ? -1ll : (long long)g));
 }
 
 // Workgroups are dispatched round-robin over the 8 XCDs (block b runs on XCD b % 8), each with
@@ -235,13 +250,16 @@ static_assert(kStatLds <= kWaveLds, "the record's reduction fits the wave's LDS 
 // entries before the scan and then streams them back as a reusing wave does, so the instance
 // carries one scan path (ICP_WALK_STREAM); 2 (NC) a first iterate without a transform (no record
 // is reused or stored: the instance carries no cache code); 0 either.
-template <bool APPLY, int NG, bool CERT, bool HALF, bool DBG, int CM = 0>
+template <bool APPLY, int NG, bool CERT, bool HALF, bool DBG, int CM = 0, bool WIDE = false>
 __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, const int lane, unsigned char* wl) {
   // previous residuals: known to the WC (yes) and NC (no) instances
   const bool have_prev = CM == 1 ? true : CM == 2 ? false : a.have_prev != 0;
   constexpr bool kDbg = DBG && kDbgCounts;
+  // a second pass (the half pass, the wide pass): queries already moved, no cache, no wave record
+  constexpr bool kSecond = HALF || WIDE;
   static_assert(NG == 1 || NG == 2 || NG == 4, "scan groups: 1, 2 or 4");
-  static_assert(!(HALF && (APPLY || CERT)), "the half pass searches moved queries");
+  static_assert(!(kSecond && (APPLY || CERT)), "the second passes search moved queries");
+  static_assert(!(HALF && WIDE), "one second pass per instance");
   const bool active = i < a.n;
   int32_t* queue = reinterpret_cast<int32_t*>(wl);
   double4* stage = reinterpret_cast<double4*>(wl);  // after the walk only
@@ -252,7 +270,7 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
   // reusing wave has its first chunk before the box is known; unused otherwise).
   const int32_t i0 = __builtin_amdgcn_readfirstlane(i);
   const uint32_t wid = (uint32_t)i0 >> 6;
-  const bool use_wc = !HALF && CM != 2 && a.wc_box != nullptr && i0 < a.n;
+  const bool use_wc = !kSecond && CM != 2 && a.wc_box != nullptr && i0 < a.n;
   // the previous match, whose fl(d2) is u (read unconditionally: an unused load costs no wait,
   // while a conditional one is waited for inside its branch)
   const int32_t prev_pos = qat(a.pos_out, active ? i : 0);
@@ -426,7 +444,7 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
         }
         wave_append_u(active && finite_q && !safe, i, u, a.fb_count + 1, a.fb_list2, a.fb_u2);
       }
-      if (!HALF) wave_record<DBG>(a, wid, lane, active, safe || !finite_q, d, pos, qx, qy, qz, wl);
+      if (!kSecond) wave_record<DBG>(a, wid, lane, active, safe || !finite_q, d, pos, qx, qy, qz, wl);
       return;
     }
     if (a.certify_prev == 1) safe = false;  // the whole wave searches
@@ -438,7 +456,7 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
   const double amax = __builtin_fmax(__builtin_fabs(qx), __builtin_fmax(__builtin_fabs(qy), __builtin_fabs(qz)));
   // |q| <= 2^100 keeps every fp32 offset of the wave finite
   const bool cand = active && finite_q && !safe && u <= 0x1p900 && amax <= 0x1p100;
-  const float r = cand ? ball_radius32(u, amax) : 0.f;
+  float r = cand ? ball_radius32(u, amax) : 0.f;  // (the wide pass shrinks it as its bounds tighten)
   const unsigned long long cmask = __ballot(cand);
   // the join rule is a heuristic (any subset may join): fp32 mean
   const float mean_r = wave_sum_f(r) * __builtin_amdgcn_rcpf((float)(cmask ? __popcll(cmask) : 1));
@@ -628,11 +646,154 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
         wave_lds_fence();
       }
   };
+  // The wide pass (WIDE): the same walk over a box of any size, in segments. A batch whose leaves
+  // would overflow the candidate list appends the ones that fit (a prefix of its leaf lanes: the
+  // inclusive sums grow with the lane) and pushes the others back on the stack (LIFO: they start
+  // the next segment); the full list is scanned by seg(count), then refilled. Every leaf meeting
+  // the box is listed in exactly one segment. Returns false when the stack overflows or one leaf
+  // holds more points than the list (nothing is then decided here: the ball search takes it).
+  // The wide pass's group spheres: per scan group (its NG kd sub-buckets of lanes), a ball around
+  // the centre of the group's box holding every joined lane's ball (|q - c| + r, rounded up). A
+  // node whose box is farther than every sphere from its centre holds no point of any ball. Far
+  // queries near a surface make boxes much larger than their balls (the box's corners cut the
+  // surface, the balls only touch it): the spheres keep the walk to what the balls reach.
+  double sph_c[NG][3], sph_r2[NG];
+  // The box is read at every batch: seg() may shrink it (a node pushed against an older, larger
+  // box is tested again when popped).
+  auto walk_seg = [&](const double& wlx, const double& wly, const double& wlz, const double& whx, const double& why,
+                      const double& whz, auto&& seg) -> bool {
+    nleaf = 0;
+    int tail = 1;
+    int32_t* wq = reinterpret_cast<int32_t*>(wl + kWaveLds + 1024);  // the wide pass's own stack
+    if (a.cells) {
+      tail = cell_starts<64, kWaveStartK>(a, wlx, wly, wlz, whx, why, whz, lane, 0, wq);
+    } else if (lane == 0) {
+      wq[0] = 0;
+    }
+    wave_lds_fence();
+    int segs = 0, listed = 0;
+    while (tail > 0) {
+      // a popped node pushes at most 8 entries (its children, or itself back): batches shrink
+      // while the stack is nearly full, so it never overflows (depth-first: the deepest entries
+      // are popped first and the stack drains)
+      int batch = (kWideQueue - tail) / 7;
+      batch = batch < 1 ? 1 : batch > 64 ? 64 : batch;
+      batch = tail < batch ? tail : batch;
+      const bool has = lane < batch;
+      const int32_t nid = has ? wq[tail - batch + lane] : 0;
+      const NodeRec* nr = a.nodes + nid;
+      NodeLoad nd;
+      nd.l01 = *reinterpret_cast<const double2*>(&nr->lo[0]);
+      nd.l2h0 = *reinterpret_cast<const double2*>(&nr->lo[2]);
+      nd.h12 = *reinterpret_cast<const double2*>(&nr->hi[1]);
+      const int2 topo = *reinterpret_cast<const int2*>(&nr->first);
+      const int32_t first = has ? topo.x : 0;
+      // the node itself against the current box (it met the box it was pushed against) and the
+      // group spheres: its squared box distance from a sphere's centre (rounding up to a few ulps,
+      // covered by the spheres' margin) at most the radius squared
+      bool live = has && nd.l01.x <= whx && nd.l2h0.y >= wlx && nd.l01.y <= why && nd.h12.x >= wly &&
+                  nd.l2h0.x <= whz && nd.h12.y >= wlz;
+      if (live) {
+        bool any = false;
+#pragma unroll
+        for (int g = 0; g < NG; g++)
+          any = any || (sph_r2[g] > 0.0 &&  // 0: a group without joined lanes (its centre is not finite)
+                        !(box_s(nd.l01.x, nd.l01.y, nd.l2h0.x, nd.l2h0.y, nd.h12.x, nd.h12.y, sph_c[g][0],
+                                sph_c[g][1], sph_c[g][2]) > sph_r2[g]));
+        live = any;
+      }
+      const uint32_t meta = live ? (uint32_t)topo.y : 0u;
+      const uint32_t kids = (live && !(meta & kLeafBit)) ? children_in_box(nd, meta & 0xffu, wlx, wly, wlz, whx, why, whz) : 0u;
+      const int lcnt = (live && (meta & kLeafBit)) ? (int)(meta & ~kLeafBit) : 0;
+      if (__ballot(lcnt > kWaveCandCap) != 0) return false;
+      int ltot;
+      const int lincl = wave_incl_scan(lcnt, &ltot);
+      const bool fit = lcnt > 0 && nleaf + lincl <= kWaveCandCap;
+      const bool back = lcnt > 0 && !fit;
+      if (fit)
+        for (int c = 0; c < lcnt; c++) plist[nleaf + lincl - lcnt + c] = first + c;
+      // the points appended: the exclusive sum at the first leaf lane that did not fit
+      const unsigned long long bm = __ballot(back);
+      const int app = bm ? __builtin_amdgcn_readlane(lincl - lcnt, __builtin_ctzll(bm)) : ltot;
+      nleaf += app;
+      listed += app;
+      const int nch = __builtin_popcount(kids) + (back ? 1 : 0);
+      int tot;
+      const int incl = wave_incl_scan(nch, &tot);
+      tail -= batch;  // the popped entries are in registers; pushes overwrite them
+      if (tail + tot > kWideQueue) {
+        if (kDbg && a.dbg && lane == 0) atomicAdd(&a.dbg[34], 1ull);
+        return false;
+      }
+      int off = tail + incl - nch;
+      if (back) wq[off++] = nid;
+      uint32_t kk = kids;
+      while (kk) {
+        const uint32_t o = (uint32_t)__builtin_ctz(kk);
+        kk &= kk - 1u;
+        wq[off++] = first + __builtin_popcount(meta & 0xffu & ((1u << o) - 1u));
+      }
+      tail += tot;
+      if (kDbg && a.dbg && lane == 0) atomicAdd(&a.dbg[5], 1ull);
+      wave_lds_fence();
+      if (bm != 0) {
+        seg(nleaf);
+        ++segs;
+        nleaf = 0;
+        wave_lds_fence();  // the segment's reads of the list are done before it is refilled
+        // a box this dense for its balls (their bounding box cuts a surface far wider than the
+        // balls do) is left to the per-query searches, with the bounds found so far
+        if (segs >= kWideSegs && tail > 0) {
+          if (kDbg && a.dbg && lane == 0) atomicAdd(&a.dbg[34], 1ull);
+          return false;
+        }
+      }
+    }
+    if (nleaf > 0) {
+      seg(nleaf);
+      ++segs;
+    }
+    if (kDbg && a.dbg && lane == 0) {
+      atomicAdd(&a.dbg[32], 1ull);
+      atomicAdd(&a.dbg[33], (unsigned long long)segs);
+      atomicAdd(&a.dbg[36], (unsigned long long)listed);
+    }
+    return true;
+  };
   bool wstore = false, reuse = false;
   double wlx = 0.0, wly = 0.0, wlz = 0.0, whx = 0.0, why = 0.0, whz = 0.0;  // B+ of a walk
   double blx = 0.0, bly = 0.0, blz = 0.0, bhx = -1.0, bhy = -1.0, bhz = -1.0;  // B (fp64) of a walking wave
   double ocx = ox_, ocy = oy_, ocz = oz_;  // the scan frame's centre (B+'s with the cache, else B's)
   double ext = 0.0;  // >= |offset| of every point inside B and every joined query, in the frame
+  auto group_spheres = [&]() {
+#pragma unroll
+    for (int g = 0; g < NG; g++) {
+      sph_c[g][0] = uniform_d(ocx + 0.5 * ((double)gl[g][0] + (double)gh[g][0]));
+      sph_c[g][1] = uniform_d(ocy + 0.5 * ((double)gl[g][1] + (double)gh[g][1]));
+      sph_c[g][2] = uniform_d(ocz + 0.5 * ((double)gl[g][2] + (double)gh[g][2]));
+    }
+    const int gq = lane / (64 / NG);
+    double cx = sph_c[0][0], cy = sph_c[0][1], cz = sph_c[0][2];
+#pragma unroll
+    for (int g = 1; g < NG; g++) {
+      cx = gq == g ? sph_c[g][0] : cx;
+      cy = gq == g ? sph_c[g][1] : cy;
+      cz = gq == g ? sph_c[g][2] : cz;
+    }
+    const double dx = qx - cx, dy = qy - cy, dz = qz - cz;
+    // |q - c| rounded up, plus the lane's radius (an upper bound already), as an fp32 key
+    const double rr = (__builtin_sqrt(dx * dx + dy * dy + dz * dz) + (double)r) * (1.0 + 0x1p-40) + 0x1p-1000;
+    int key = join ? __float_as_int((float)rr * (1.0f + 0x1p-22f)) : 0;  // >= 0: int order is float order
+    key = rows_max_i(key);
+    if (NG <= 2) key = halves_max_i(key);
+    if (NG == 1) key = wave_max_from_halves(key);
+#pragma unroll
+    for (int g = 0; g < NG; g++) {
+      const float R = __int_as_float(__builtin_amdgcn_readlane(key, (64 / NG) * g + 64 / NG - 1));
+      sph_r2[g] = (double)R * (double)R * (1.0 + 0x1p-40);  // 0 for a group without joined lanes
+    }
+  };
+
   WaveBox* wb = nullptr;
   float4* wents = nullptr;
   if (jm != 0) {
@@ -707,7 +868,8 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
       whx = uniform_d(bhx + (m + dhx));
       why = uniform_d(bhy + (m + dhy));
       whz = uniform_d(bhz + (m + dhz));
-      walk(wlx, wly, wlz, whx, why, whz);
+      // (the wide pass walks B in segments during its scan, phase 4)
+      if (!WIDE) walk(wlx, wly, wlz, whx, why, whz);
       if (overflow && keep) {
         // B+ holds too many points: walk again with a quarter of the margin and the lead, and
         // store that list (an overflowing wave that stored nothing would overflow again at every
@@ -738,7 +900,7 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
       // |offset| <= ext for every point inside B and every joined query (B lies in the frame box)
       ext = dmax_(dmax_(dmax_(bhx - ocx, ocx - blx), dmax_(bhy - ocy, ocy - bly)), dmax_(bhz - ocz, ocz - blz)) *
             (1.0 + 0x1p-40);
-      if (!overflow && nleaf > 0) {
+      if (!overflow && (WIDE || nleaf > 0)) {
         // the group boxes and the queries' offsets again, in the frame
         reduce((float)(qx - ocx), (float)(qy - ocy), (float)(qz - ocz));
         group_bounds((float)(ext * 0x1p-20));
@@ -765,6 +927,7 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
   // balls; an overflowing half hands its queries to the ball search.
   bool deferred = false;
   if (overflow) {
+    if (!kSecond && lane == 0) atomicAdd(a.fb_count + 6, 1u);  // the iteration record's n_wide
     if (!HALF && CM != 1 && a.fb_list3 != nullptr) {  // the half pass: first iterates only
       // entries (half id, mask of its deferred lanes): the half pass searches exactly these
       const unsigned long long dm = __ballot(join);
@@ -782,6 +945,21 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
           a.fb_list3[2 * at + 1] = (int32_t)(uint32_t)(dm >> 32);
         }
         if (kDbg && a.dbg) atomicAdd(&a.dbg[16], (unsigned long long)nh);
+      }
+    } else if (!WIDE && a.fb_list4 != nullptr) {
+      // the wide pass (k_nn_wide) searches the joined lanes again with the same box, walked and
+      // scanned in segments: (first query of the wave or half, lane mask) per entry
+      const unsigned long long dm = __ballot(join);
+      deferred = join;
+      if (dm != 0) {
+        const int fl = __builtin_ctzll(dm);
+        const int32_t base = __builtin_amdgcn_readlane(i, fl) - fl;  // i = base + lane
+        if (lane == 0) {
+          const unsigned at = atomicAdd(a.fb_count + 5, 1u);
+          a.fb_list4[3 * at] = base;
+          a.fb_list4[3 * at + 1] = (int32_t)(uint32_t)dm;
+          a.fb_list4[3 * at + 2] = (int32_t)(uint32_t)(dm >> 32);
+        }
       }
     }
     join = false;
@@ -804,23 +982,15 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
     if (wstore) {
       int wcount = 0;
       double4 nxtp = make_double4(0.0, 0.0, 0.0, 0.0);
-      if (lane < nleaf) {
-        const int32_t g = plist[lane];
-        const TgtPt* p = a.pts + g;
-        const double2 xy = *reinterpret_cast<const double2*>(&p->x);
-        nxtp = make_double4(xy.x, xy.y, p->z, __longlong_as_double((long long)g));
-      }
+      // a copy of an earlier point (TgtPt::sep's sign) is never stored: its twin is the reference's
+      // answer whenever it would be (id -1 below)
+      if (lane < nleaf) nxtp = load_cand(a.pts, plist[lane]);
       for (int base = 0; base < nleaf; base += 64) {
         const double4 cur = nxtp;
         const int nb = base + 64;
-        if (nb + lane < nleaf) {
-          const int32_t g = plist[nb + lane];
-          const TgtPt* p = a.pts + g;
-          const double2 xy = *reinterpret_cast<const double2*>(&p->x);
-          nxtp = make_double4(xy.x, xy.y, p->z, __longlong_as_double((long long)g));
-        }
+        if (nb + lane < nleaf) nxtp = load_cand(a.pts, plist[nb + lane]);
         const bool inp = base + lane < nleaf && cur.x >= wlx && cur.x <= whx && cur.y >= wly && cur.y <= why &&
-                         cur.z >= wlz && cur.z <= whz;
+                         cur.z >= wlz && cur.z <= whz && __double_as_longlong(cur.w) >= 0;
         const unsigned long long pm = __ballot(inp);
         if (inp)
           wents[wcount + mask_rank(pm)] = make_float4((float)(cur.x - ocx), (float)(cur.y - ocy), (float)(cur.z - ocz),
@@ -839,7 +1009,11 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
   }
   const int npts = nleaf;
   int scanned_pts = 0;
-  bool need64 = __ballot(join) != 0 && npts > 0;
+  bool need64 = __ballot(join) != 0 && (WIDE || npts > 0);
+  // the wide pass: lanes it leaves undecided (no certificate, or a walk that overflowed) take the
+  // ball search with the tightest upper bound it found (gw: the fp64 fl(d2) of a scanned point)
+  bool wide_lane = false;
+  double gw = u;
   if (a.scan32 && need64) {
     if (ext >= 0x1p-40 && ext <= 0x1p60) {
       constexpr int LG = 64 / NG;  // lanes of a group
@@ -855,7 +1029,8 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
       // Pair k of group g at k NG + g: the groups interleaved (each group's pairs contiguous costs
       // two more spilled registers)
       auto blk = [](int k, int g) { return k * NG + g; };
-      float* stage32 = reinterpret_cast<float*>(wl);
+      // (the wide pass keeps its walk's stack through the scan: its staging area follows the list)
+      float* stage32 = reinterpret_cast<float*>(wl + (WIDE ? kWaveLds : 0));
       // Selection keys: the fp32 squared distance with its low 6 bits replaced by the point's slot
       // in the segment (v_bfi), so that the two smallest are kept by two med3 per point and the
       // winner is found from its slot once per round. A key is within 63 ulps of its value, and
@@ -901,8 +1076,9 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
       // into the group's segment; `next` issues the following chunk's loads once this one is
       // staged; then the lockstep scan. Later rounds (more than S points of one group in one
       // chunk, rare) test again rather than keep NG ranks and masks live.
+      int seg_n = npts;  // points of the list being scanned (the wide pass: of its segment)
       auto chunk = [&](int base, float vx, float vy, float vz, float vw, auto&& next) {
-        const bool valid = base + lane < npts;
+        const bool valid = base + lane < seg_n;
         int cn[NG];
         int maxc = 0;
         auto stage_round = [&](int r0, bool count) {
@@ -1053,18 +1229,18 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
         scan_round();
       } else {
         int wcount = 0;  // entries stored to the cache (points inside B+)
+        auto gather_scan = [&](const int np) {
+        seg_n = np;
         double4 nxtp = make_double4(0.0, 0.0, 0.0, 0.0);
-        if (lane < npts) {
-          const int32_t g = plist[lane];
-          const TgtPt* p = a.pts + g;
-          const double2 xy = *reinterpret_cast<const double2*>(&p->x);
-          nxtp = make_double4(xy.x, xy.y, p->z, __longlong_as_double((long long)g));
-        }
-        for (int base = 0; base < npts; base += 64) {
-          const float vx = (float)(nxtp.x - ocx), vy = (float)(nxtp.y - ocy), vz = (float)(nxtp.z - ocz);
+        if (lane < np) nxtp = load_cand(a.pts, plist[lane]);
+        for (int base = 0; base < np; base += 64) {
+          // a copy of an earlier point is staged far outside every group box (never scanned)
+          const bool cp = __double_as_longlong(nxtp.w) < 0;
+          const float vx = cp ? 0x1p62f : (float)(nxtp.x - ocx), vy = cp ? 0x1p62f : (float)(nxtp.y - ocy),
+                      vz = cp ? 0x1p62f : (float)(nxtp.z - ocz);
           const float vw = __int_as_float((int)__double_as_longlong(nxtp.w));
           if (wstore) {
-            const bool inp = base + lane < npts && nxtp.x >= wlx && nxtp.x <= whx && nxtp.y >= wly &&
+            const bool inp = base + lane < np && !cp && nxtp.x >= wlx && nxtp.x <= whx && nxtp.y >= wly &&
                              nxtp.y <= why && nxtp.z >= wlz && nxtp.z <= whz;
             const unsigned long long pm = __ballot(inp);
             if (inp) wents[wcount + mask_rank(pm)] = make_float4(vx, vy, vz, vw);
@@ -1072,13 +1248,39 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
           }
           chunk(base, vx, vy, vz, vw, [&]() {
             const int nb = base + 64;
-            if (nb + lane < npts) {
-              const int32_t g = plist[nb + lane];
-              const TgtPt* p = a.pts + g;
-              const double2 xy = *reinterpret_cast<const double2*>(&p->x);
-              nxtp = make_double4(xy.x, xy.y, p->z, __longlong_as_double((long long)g));
-            }
+            if (nb + lane < np) nxtp = load_cand(a.pts, plist[nb + lane]);
           });
+        }
+        if constexpr (WIDE) {
+          // The lane's winner so far is a point: its fl(d2) bounds the nearest one's. The balls
+          // shrink to the tighter bounds, and the box (in the same frame, rounded outwards) and
+          // the group boxes with them: every point of a final ball lies in every earlier box, so
+          // it is still listed and scanned; the rest of the walk visits less.
+          if (join && p1 >= 0) {
+            const TgtPt* p = a.pts + p1;
+            const double dx = p->x - qx, dy = p->y - qy, dz = p->z - qz;
+            const double d2 = dx * dx + dy * dy + dz * dz;
+            u = d2 < u ? d2 : u;
+          }
+          r = join ? ball_radius32(u, amax) : 0.f;
+          reduce((float)(qx - ocx), (float)(qy - ocy), (float)(qz - ocz));
+          blx = uniform_d(box_lo(ocx, funkey(wkl[0])));
+          bly = uniform_d(box_lo(ocy, funkey(wkl[1])));
+          blz = uniform_d(box_lo(ocz, funkey(wkl[2])));
+          bhx = uniform_d(box_hi(ocx, funkey(wkh[0])));
+          bhy = uniform_d(box_hi(ocy, funkey(wkh[1])));
+          bhz = uniform_d(box_hi(ocz, funkey(wkh[2])));
+          group_bounds((float)(ext * 0x1p-20));
+          group_spheres();
+        }
+        };
+        if constexpr (WIDE) {
+          // B itself (fp64, rounded outwards) in segments; a stack overflow leaves every joined
+          // lane to the ball search
+          group_spheres();
+          if (!walk_seg(blx, bly, blz, bhx, bhy, bhz, gather_scan)) wide_lane = join;
+        } else {
+          gather_scan(npts);
         }
         if (wstore) {
           store_header(wcount);
@@ -1099,8 +1301,24 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
       // bound of the rest: the per-lane search takes it, as after an fp64 scan); or a certified
       // winner within the guess. Anything else (a near tie, or a winner beyond u while another
       // point may be within it) re-scans the wave in fp64, which decides as the fp64 scan does.
+      if constexpr (WIDE) {
+        // no fp64 re-scan over segments: a lane that is not certified takes the ball search, with
+        // its winner's fl(d2) as the bound when that is below its guess (any scanned point's is
+        // an upper bound of the nearest one's)
+        const bool dec = !wide_lane && join && p1 >= 0 && b64 <= u && certified(b64, lb2, a.init_best);
+        if (join && p1 >= 0 && b64 < gw) gw = b64;
+        wide_lane = join && !dec;
+        if (kDbg && a.dbg) {
+          const unsigned long long um = __ballot(wide_lane);
+          if (lane == 0) atomicAdd(&a.dbg[35], (unsigned long long)__popcll(um));
+        }
+        best = dec ? b64 : __builtin_inf();
+        second = lb2;
+        bpos = p1;
+        need64 = false;
+      }
       const bool ok = !join || p1 < 0 || (!(b64 <= u) && lb2 > u) || (b64 <= u && certified(b64, lb2, a.init_best));
-      if (__ballot(!ok) == 0) {
+      if (!WIDE && __ballot(!ok) == 0) {
         best = b64;
         second = lb2;
         bpos = p1;
@@ -1228,6 +1446,8 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
       pos = a.pos0;
       d = residual_to(a.pts, pos, qx, qy, qz);
       written = true;
+    } else if (WIDE && wide_lane) {
+      to_lane = true;  // undecided by the wide pass (gw bounds its nearest distance)
     } else if (join && !(best <= u)) {
       to_lane = true;  // the guess did not cover the nearest point: search this one per lane
     } else if (join) {
@@ -1244,8 +1464,9 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
   }
   wave_append(to_exact, i, a.fb_count, a.fb_list);
   const bool covered = !(join && !(best <= u));
-  wave_append_u(to_lane, i, covered ? u : __builtin_inf(), a.fb_count + 1, a.fb_list2, a.fb_u2);
-  if (!HALF)
+  wave_append_u(to_lane, i, (WIDE && wide_lane) ? gw : covered ? u : __builtin_inf(), a.fb_count + 1, a.fb_list2,
+                a.fb_u2);
+  if (!kSecond)
     wave_record<DBG>(a, wid, lane, active, safe || written, safe ? __builtin_sqrt(u) : d, safe ? prev_pos : pos, qx,
                      qy, qz, wl);
 #if ICP_PHASE_CLOCKS
@@ -1311,6 +1532,35 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
   }
 }
 
+// The wide pass: every wave takes an overflowed wave (or half) from the list (grid-stride; the
+// list is complete when this kernel starts): its deferred lanes search again with the same box,
+// which the wave walks and scans in segments of up to kWaveCandCap points (walk_seg). Its LDS
+// area holds the walk's stack, the list and a staging area of its own (the stack stays live
+// through each segment's scan).
+constexpr int kWideLds = kWaveLds + 1024 + kWideQueue * 4;
+// (6 KB of LDS per wave admits ~6.5 waves per SIMD: compiled for 6, 80 VGPRs)
+#ifndef ICP_WIDE_WPE
+#define ICP_WIDE_WPE 6
+#endif
+template <int NG, bool DBG>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ICP_WIDE_WPE, ICP_WIDE_WPE))) k_nn_wide(NNLaunch a) {
+  if (a.loop && a.loop->core.done) return;
+  extern __shared__ __attribute__((aligned(16))) unsigned long long lds_raw[];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  unsigned char* wl = reinterpret_cast<unsigned char*>(lds_raw) + wv * kWideLds;
+  const unsigned cnt = a.fb_count[5];
+  const unsigned waves = gridDim.x * (blockDim.x >> 6);
+  for (unsigned j = blockIdx.x * (blockDim.x >> 6) + wv; j < cnt; j += waves) {
+    const int64_t base = a.fb_list4[3 * j];
+    const unsigned long long mask =
+        (unsigned long long)(uint32_t)a.fb_list4[3 * j + 1] | (unsigned long long)(uint32_t)a.fb_list4[3 * j + 2] << 32;
+    const int64_t q = base + lane;
+    const int32_t i = (((mask >> lane) & 1ull) && q < a.n) ? (int32_t)q : (int32_t)a.n;
+    wave_lds_fence();  // the previous entry's LDS reads are done
+    wave_search<false, NG, false, false, DBG, 0, true>(a, i, lane, wl);
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // The ball search: four queries per wave, one 16-lane group (a DPP row) each. The list's queries
 // are latency-bound walks of a few dependent rounds, so four in flight per wave hide four times
@@ -1361,6 +1611,8 @@ __device__ __forceinline__ bool lane_query(const NNLaunch& a, int64_t i, unsigne
     a.dist_out[i] = __builtin_sqrt(best);
   } else {
     exact_query(a, i, st, bs);
+    atomicAdd(a.fb_count + 3, 1u);  // a DFS finish of the ball search
+    if (a.dbg) atomicAdd(&a.dbg[38], 1ull);
   }
   return true;
 }
@@ -1377,7 +1629,8 @@ __device__ __forceinline__ bool lane_query(const NNLaunch& a, int64_t i, unsigne
 #define ICP_LANE_BUDGET 64
 #endif
 constexpr int kLaneBudget = ICP_LANE_BUDGET;
-constexpr int kBBStack = 2048;  // the cooperative search's node stack (int32 in LDS)
+constexpr int kBBStack = 2048;  // the cooperative search's node stack (int32 in LDS), the last
+constexpr int kBBPts = 256;     // kBBPts entries of which hold a step's leaf points
 
 // The wave-cooperative certified search of one query (every lane of the wave): branch and bound
 // over the octree, up to 64 nodes per step (one per lane, LIFO), each node re-tested against the
@@ -1396,6 +1649,7 @@ __device__ __forceinline__ bool wave_bb(const NNLaunch& a, int64_t i, double u, 
   const double qx = a.x[i], qy = a.y[i], qz = a.z[i];
   double best = __builtin_inf(), second = __builtin_inf();
   int32_t bpos = 0x7fffffff;
+  int32_t* plist = stack + (kBBStack - kBBPts);
   double thr = (u <= 0x1p900) ? u * (1.0 + kFastPrune) : __builtin_inf();
   int steps = 0, passes = 0;
   bool over = false;
@@ -1431,29 +1685,56 @@ __device__ __forceinline__ bool wave_bb(const NNLaunch& a, int64_t i, double u, 
       const uint32_t meta = (uint32_t)topo.y;
       // pushed against an older (larger) bound: test the node itself again
       const bool live = has && !(box_s(l01.x, l01.y, l2h0.x, l2h0.y, h12.x, h12.y, qx, qy, qz) > thr);
-      uint32_t kids = 0;
-      if (live && (meta & kLeafBit)) {
-        const int32_t cnt = (int32_t)(meta & ~kLeafBit);
-        for (int32_t k = 0; k < cnt; k++) {
-          const TgtPt* p = a.pts + topo.x + k;
+      const bool lf = live && (meta & kLeafBit);
+      const uint32_t kids = (live && !lf) ? children_in_ball(rr, meta & 0xffu, qx, qy, qz, thr) : 0u;
+      // The step's leaf points, flat: listed in LDS kBBPts at a time and scanned kBBPts / 64 per
+      // lane with all their loads in flight together (a leaf scanned by its own lane was ~10
+      // dependent round trips per step). Each point is scanned by one lane: the per-lane best and
+      // second reduce to the wave's exactly as before.
+      const int lcnt = lf ? (int)(meta & ~kLeafBit) : 0;
+      int ltot;
+      const int lfirst = wave_incl_scan(lcnt, &ltot) - lcnt;
+      for (int base = 0; base < ltot; base += kBBPts) {
+        for (int k = 0; k < lcnt; k++) {
+          const int f = lfirst + k - base;
+          if (f >= 0 && f < kBBPts) plist[f] = topo.x + k;
+        }
+        wave_lds_fence();
+        const int m = ltot - base < kBBPts ? ltot - base : kBBPts;
+        constexpr int P = kBBPts / 64;
+        double px[P], py[P], pz[P];
+        int32_t pid[P];
+#pragma unroll
+        for (int t = 0; t < P; t++) {
+          pid[t] = t * 64 + lane < m ? plist[t * 64 + lane] : -1;
+          const TgtPt* p = a.pts + (pid[t] >= 0 ? pid[t] : 0);
           const double2 pxy = *reinterpret_cast<const double2*>(&p->x);
-          const double dx = pxy.x - qx, dy = pxy.y - qy, dz = p->z - qz;
+          const double2 pzw = *reinterpret_cast<const double2*>(&p->z);
+          px[t] = pxy.x;
+          py[t] = pxy.y;
+          pz[t] = pzw.x;
+          pid[t] = tgt_copy_word(pzw.y) ? -1 : pid[t];  // a copy: its earlier twin is scanned
+        }
+#pragma unroll
+        for (int t = 0; t < P; t++) {
+          const double dx = px[t] - qx, dy = py[t] - qy, dz = pz[t] - qz;
           const double d2 = dx * dx + dy * dy + dz * dz;
-          if (d2 < best) {
-            second = best;
-            best = d2;
-            bpos = topo.x + k;
-          } else if (d2 < second) {
-            second = d2;
+          if (pid[t] >= 0) {
+            if (d2 < best) {
+              second = best;
+              best = d2;
+              bpos = pid[t];
+            } else if (d2 < second) {
+              second = d2;
+            }
           }
         }
-      } else if (live) {
-        kids = children_in_ball(rr, meta & 0xffu, qx, qy, qz, thr);
+        wave_lds_fence();  // the list's reads are done before the next round rewrites it
       }
       const int nch = __builtin_popcount(kids);
       int tot;
       const int incl = wave_incl_scan(nch, &tot);
-      if (tail + tot > kBBStack) {
+      if (tail + tot > kBBStack - kBBPts) {
         over = true;
         break;
       }
@@ -1479,7 +1760,7 @@ __device__ __forceinline__ bool wave_bb(const NNLaunch& a, int64_t i, double u, 
   if (a.dbg && lane == 0) {
     atomicAdd(&a.dbg[27], 1ull);
     atomicAdd(&a.dbg[28], (unsigned long long)steps);
-    if (over) atomicAdd(&a.dbg[23], 1ull);
+    if (over) atomicAdd(&a.dbg[37], 1ull);
   }
   if (over) return false;
   // the wave's best, and its second: the smallest of the other lanes' bests and the best lane's
@@ -1495,6 +1776,8 @@ __device__ __forceinline__ bool wave_bb(const NNLaunch& a, int64_t i, double u, 
     }
   } else if (lane == 0) {
     exact_query(a, i, dfs_st, 1);
+    atomicAdd(a.fb_count + 3, 1u);  // a DFS finish of the ball search (icp_iter_stats.n_fallback)
+    if (a.dbg) atomicAdd(&a.dbg[38], 1ull);
   }
   return true;
 }
@@ -1547,8 +1830,11 @@ __global__ void __launch_bounds__(64) k_nn_ball(NNLaunch a) {
       const int64_t iq = __builtin_amdgcn_readlane(e, k) & 0x3fffffff;
       const double uq = readlane_d(qu, k);
       // the stack in the DFS columns' area (free now); the fallback DFS after it, in the same area
-      if (!wave_bb(a, iq, uq, reinterpret_cast<int32_t*>(lds_raw), lds_raw, lane) && lane == 0)
+      if (!wave_bb(a, iq, uq, reinterpret_cast<int32_t*>(lds_raw), lds_raw, lane) && lane == 0) {
         exact_query(a, iq, lds_raw, 1);
+        atomicAdd(a.fb_count + 3, 1u);
+        if (a.dbg) atomicAdd(&a.dbg[38], 1ull);
+      }
       wave_lds_fence();
     }
     qn = 0;
@@ -1566,13 +1852,20 @@ __global__ void __launch_bounds__(64) k_nn_ball(NNLaunch a) {
   // 4's window 4 % (its 15k-query lists of easy balls).
   // (icp_hip_config.ball_mode: 0 this rule, 1 the ball walk always, 2 direct always)
   if (a.ball_mode == 2 || (a.ball_mode == 0 && (cnt <= gridDim.x || cnt > 4u * gridDim.x))) {
-    for (unsigned j = blockIdx.x; j < cnt; j += gridDim.x) {
+    unsigned taken = 0;
+    for (unsigned j = blockIdx.x; j < cnt; j += gridDim.x, ++taken) {
       const int64_t i = a.fb_list2[j];
       const double u = a.fb_u2[j];
-      if (!wave_bb(a, i, u, reinterpret_cast<int32_t*>(lds_raw), lds_raw, lane) && lane == 0)
+      if (!wave_bb(a, i, u, reinterpret_cast<int32_t*>(lds_raw), lds_raw, lane) && lane == 0) {
         exact_query(a, i, lds_raw, 1);
+        atomicAdd(a.fb_count + 3, 1u);
+        if (a.dbg) atomicAdd(&a.dbg[38], 1ull);
+      }
       wave_lds_fence();
     }
+    // the queries taken by the cooperative search count as follow-up searches, as after the ball
+    // walk (icp_iter_stats.n_lane_search)
+    if (lane == 0 && taken > 0) atomicAdd(a.fb_count + 2, taken);
     return;
   }
   for (unsigned j0 = blockIdx.x * kBallGroups; j0 < cnt; j0 += gridDim.x * kBallGroups) {
@@ -1943,6 +2236,28 @@ hipError_t launch_nn(const NNLaunch& a, hipStream_t s) {
       default: return hipErrorInvalidValue;
     }
   }
+  // the wide pass over the overflowed waves and halves (queries already moved: no transform)
+  if (a.fb_list4) {
+    NNLaunch w = a;
+    w.apply = 0;
+    w.wc_box = nullptr;
+    w.wc_ents = nullptr;
+    const int64_t wb = (a.n + 255) / 256;
+    const unsigned ggrid = (unsigned)(wb < 2048 ? wb : 2048);
+    const size_t gshm = (size_t)(256 / 64) * kWideLds;
+    auto wide = [&](auto kern) {
+      hipExtLaunchKernelGGL(kern, dim3(ggrid), dim3(256), (uint32_t)gshm, s, nullptr, nullptr, 0u, w);
+    };
+    switch (a.scan_groups + (dbg ? 8 : 0)) {
+      case 1: wide(k_nn_wide<1, false>); break;
+      case 2: wide(k_nn_wide<2, false>); break;
+      case 4: wide(k_nn_wide<4, false>); break;
+      case 9: wide(k_nn_wide<1, true>); break;
+      case 10: wide(k_nn_wide<2, true>); break;
+      case 12: wide(k_nn_wide<4, true>); break;
+      default: return hipErrorInvalidValue;
+    }
+  }
   // the follow-up lists are short (the ball list ~0.1 % of the queries, the exact list usually
   // empty): one launch of 64-thread blocks, grid-stride over them; LDS for the group stacks and
   // lists or, before them, one DFS stack of `levels` entries per thread
@@ -1952,6 +2267,9 @@ hipError_t launch_nn(const NNLaunch& a, hipStream_t s) {
   NNLaunch b = a;
   if (bshm < (size_t)kBBStack * sizeof(int32_t)) bshm = (size_t)kBBStack * sizeof(int32_t);  // wave_bb's stack
   b.ball_queue_off = (int32_t)bshm;  // the follow-up queue (64 entries + guesses) after the stacks and lists
+  // after the wide pass the list holds what it left: far queries (lanes that joined no box, and
+  // lanes the wide pass could not certify, with its bounds): whole queries per wave
+  if (a.fb_list4 && b.ball_mode == 0) b.ball_mode = 2;
   bshm += 64 * (sizeof(int32_t) + sizeof(double));
   hipExtLaunchKernelGGL(k_nn_ball, dim3((unsigned)(bq < 8192 ? bq : 8192)), dim3(64), (uint32_t)bshm, s, nullptr,
                         nullptr, 0u, b);

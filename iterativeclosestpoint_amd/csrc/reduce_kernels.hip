@@ -450,6 +450,7 @@ __device__ void loop_step(LoopDev* L, const IterDev& r, LoopRec* out) {
     L->core = core;
   }
   out->outcome = outcome;
+  out->pad[0] = (int32_t)r.n_wide;
   for (int k = 0; k < 16; k++) {
     out->T[k] = core.T[k];
     out->Tc[k] = core.Tc[k];
@@ -479,7 +480,8 @@ __device__ void finalize_cov_publish(IterDev* it, const CovMoments& g, IterPubli
     rec->pad[0] = (double)(pub.lists[0] + pub.lists[3]);
     rec->pad[1] = (double)pub.lists[1];
     rec->pad[2] = (double)pub.lists[2];
-    for (int k = 0; k < 5; k++) pub.lists[k] = 0u;  // + the half list of the wave search
+    rec->n_wide = (double)pub.lists[6];
+    for (int k = 0; k < 7; k++) pub.lists[k] = 0u;  // + the half and wide lists, overflowed waves
     it->c_global = rec->c_global;
     it->rmse = rec->rmse;
     band_next(it);

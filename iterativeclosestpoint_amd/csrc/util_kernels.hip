@@ -60,9 +60,33 @@ __global__ void k_gather_deinterleave(const double* aos, const int32_t* perm, do
   z[i] = aos[3 * j + 2];
 }
 
+// The copy flag of the leaf-ordered target (TgtPt::sep's sign bit, kCopyWindow): a point whose
+// coordinates equal an earlier point's among the kCopyWindow points before it. Identical points
+// share a leaf (the same octant at every split), so the earlier one comes first in the leaf's
+// order, and the reference's strict < keeps it: a flagged copy is never the answer, and its
+// distance is its earlier twin's. A copy further back stays unflagged (only a search's shortcut
+// is lost; a max-depth leaf of many points).
+__global__ void k_mark_copies(TgtPt* pts, int64_t n) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  const double x = pts[j].x, y = pts[j].y, z = pts[j].z;
+  bool copy = false;
+  for (int m = 1; m <= kCopyWindow && j - m >= 0 && !copy; m++) {
+    const TgtPt& p = pts[j - m];
+    copy = p.x == x && p.y == y && p.z == z;
+  }
+  if (copy) pts[j].sep = -0.0f;  // a copy's separation is 0 (certify_prev): the sign is the flag
+}
+
 inline unsigned grid_for(int64_t n, int bs) { return (unsigned)((n + bs - 1) / bs); }
 
 }  // namespace
+
+hipError_t launch_mark_copies(TgtPt* pts, int64_t n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_mark_copies, dim3(grid_for(n, 256)), dim3(256), 0, s, pts, n);
+  return hipGetLastError();
+}
 
 hipError_t launch_gather_deinterleave(const double* aos, const int32_t* perm, double* x, double* y, double* z,
                                       int64_t n, hipStream_t s) {

@@ -67,7 +67,7 @@ def test_create_ex_validates_config_without_a_gpu(icp):
     cfg = icp.config()
     assert cfg.no_warmup == 0 and cfg.config_version == 3
     assert icp.HipConfig.config_version.offset == 0  # the version word first: checked before the copy
-    for field, bad in (("no_warmup", 2), ("ball_mode", 3), ("peer_timeout_ms", -1), ("scan_groups", 3),
+    for field, bad in (("no_warmup", 2), ("ball_mode", 3), ("wide_pass", 3), ("peer_timeout_ms", -1), ("scan_groups", 3),
                        ("config_version", 2), ("config_version", 0)):
         c = icp.config()
         setattr(c, field, bad)
@@ -82,7 +82,7 @@ def test_create_ex_rejects_nonzero_reserved_words(icp):
     import ctypes as C
     L = icp.lib()
     h = C.c_void_p()
-    for k in range(4):
+    for k in range(3):
         c = icp.config()
         c.reserved[k] = 1
         assert L.icp_hip_create_ex(C.byref(h), 0, C.byref(c)) == icp.EINVAL

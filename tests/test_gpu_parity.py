@@ -286,12 +286,14 @@ def test_scan32_matches_fp64_scan(icp, n, cfg):
 
     a = run(None)
     b = run(cfg)
-    for (ia, da, fa, ba), (ib, db, fb, bb) in zip(a, b):
+    for it, ((ia, da, fa, ba), (ib, db, fb, bb)) in enumerate(zip(a, b)):
         np.testing.assert_array_equal(ia, ib)
         np.testing.assert_array_equal(da, db)
         assert fa == fb
-        # the same candidate sets (the candidate cache's enlarged boxes overflow other waves)
-        if set(cfg) <= {"scan32", "octree_builder", "scan_groups", "xcd_blocks"}:
+        # the same candidate sets (the candidate cache's enlarged boxes overflow other waves; the
+        # first iterate's wide pass, which takes overflowed halves instead of the ball search,
+        # runs with the fp32 scan only)
+        if set(cfg) <= {"octree_builder", "scan_groups", "xcd_blocks"} or (set(cfg) <= {"scan32"} and it > 0):
             assert ba == bb
 
 

@@ -95,3 +95,40 @@ def test_ball_modes_agree(icp, oracle, scene, which):
     oidx, od = oracle.OracleTree(tgt).nn(out[0][3], init_best=oracle.DBL_MAX)
     np.testing.assert_array_equal(out[0][1], oidx)
     np.testing.assert_array_equal(out[0][2], od)
+
+
+@pytest.mark.parametrize("which", ["scene", "blob"])
+def test_wide_pass_modes_agree(icp, oracle, scene, which):
+    """The wide pass (config.wide_pass: 1 never, 2 always, 0 the rule; k_nn_wide walks and scans an
+    overflowed wave's box in segments) against the ball search taking those queries: the same
+    correspondences, residuals and statistics bit for bit over 4 iterates (every iterate's
+    correspondences checked against the oracle with the pass always on), also without the half
+    pass of the first iterate."""
+    if which == "scene":
+        tgt, src, _ = scene
+    else:
+        tgt, src, _ = icp.synth_pair(300_000, yaw_deg=3.0)
+    tree = oracle.OracleTree(tgt)
+    out = {}
+    for key in ((0, 1), (1, 1), (2, 1), (2, 0)):
+        wide, halves = key
+        with icp.Context(0, icp.config(wide_pass=wide, overflow_halves=halves)) as ctx:
+            ctx.set_target(tgt, 10, 20, icp.RULES_ENGINE)
+            ctx.set_source(src)
+            T, recs, corr = None, [], []
+            for it in range(4):
+                st = ctx.iterate(T, it, icp.RULES_ENGINE, 3.0)
+                recs.append((st.valid, st.mean, st.std, st.rmse, tuple(st.H)))
+                idx, d = ctx.get_correspondences()
+                corr.append((idx, d))
+                if key == (2, 1):
+                    oidx, od = tree.nn(ctx.get_source(), init_best=oracle.DBL_MAX)
+                    np.testing.assert_array_equal(idx, oidx, err_msg=f"iterate {it}")
+                    np.testing.assert_array_equal(d, od, err_msg=f"iterate {it}")
+                T = icp.best_fit_from_stats(st)
+            out[key] = (recs, corr)
+    for key in out:
+        assert out[key][0] == out[(1, 1)][0], key
+        for (i0, d0), (i1, d1) in zip(out[key][1], out[(1, 1)][1]):
+            np.testing.assert_array_equal(i0, i1)
+            np.testing.assert_array_equal(d0, d1)

@@ -55,10 +55,12 @@ def per_dispatch(prof, sub):
 
 def main():
     prof, n, world = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
+    # the profiled workload (bench.py workload_key): a profile counts only for the same data
+    workload = sys.argv[4] if len(sys.argv) > 4 else "blob|q=0.0|dup=1"
     from pathlib import Path
     sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
     from bench import search_source_sha1
-    out = {"kernel": KERNEL, "n": n, "world": world, "search_src_sha1": search_source_sha1()}
+    out = {"kernel": KERNEL, "n": n, "world": world, "workload": workload, "search_src_sha1": search_source_sha1()}
     # the kernel's durations over the profiled workload's dispatches (largest grid; see per_dispatch)
     tr = [r for r in rows(f"{prof}/trace/**/*kernel_trace.csv") if KERNEL in r.get("Kernel_Name", "")]
     if tr:

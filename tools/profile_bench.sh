@@ -11,7 +11,8 @@ REPO=$(pwd)
 OUT=$REPO/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-BENCH="$REPO/bench.py --points $N --no-cpu-baseline --no-parity --no-registration"
+# BENCH_EXTRA: workload arguments of bench.py (e.g. --scene); WORKLOAD: its bench.py workload_key
+BENCH="$REPO/bench.py --points $N --no-cpu-baseline --no-parity --no-registration ${BENCH_EXTRA:-}"
 cd /tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o "$TAG" -- \
   python3 $BENCH --steps $STEPS --warmup $WARMUP > "$OUT/bench_traced.json" 2> "$OUT/trace.err" || exit $?
@@ -26,5 +27,5 @@ timeout -k 10 600 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv -
 timeout -k 10 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pmc_sq" -o "$TAG" -- \
   python3 $BENCH --steps $STEPS --warmup $WARMUP > /dev/null 2> "$OUT/pmc_sq.err" || exit $?
 cd "$REPO"
-python3 tools/pmc_traffic.py "$OUT" "$N" 1 > "$OUT/traffic.json"
+python3 tools/pmc_traffic.py "$OUT" "$N" 1 "${WORKLOAD:-blob|q=0.0|dup=1}" > "$OUT/traffic.json"
 cat "$OUT/traffic.json"

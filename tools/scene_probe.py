@@ -25,7 +25,9 @@ for a in sys.argv[3:]:
     else:
         kw[k] = float(v) if "." in v or "e" in v else int(v)
 tgt, src, _ = icp.synth_scene(n, **kw)
-with icp.Context(0, icp.config(debug_counters=1, timing_stride=1, **cfg)) as ctx:
+base = {"debug_counters": 1, "timing_stride": 1}
+base.update(cfg)  # e.g. cfg.debug_counters=0: the product instances' times (no counter atomics)
+with icp.Context(0, icp.config(**base)) as ctx:
     ctx.set_target(tgt, 10, 20, icp.RULES_ENGINE)
     ctx.set_source(src)
     # the engine's own loop (icp_session_step: the reference's increments and stops)
@@ -40,7 +42,8 @@ with icp.Context(0, icp.config(debug_counters=1, timing_stride=1, **cfg)) as ctx
                "rmse": None if rec is None else rec.rmse}
         for k in ("waves", "overflow_waves", "not_joined", "not_covered", "ball_overflow", "ball_points",
                   "fp64_scan_waves", "cache_hits", "scan_pairs", "staged_points", "bb_queries", "bb_steps",
-                  "lane_handed", "bb_overflow"):
+                  "lane_handed", "bb_overflow", "wide_waves", "wide_segments", "wide_stack", "wide_undecided",
+                  "wide_points", "lane_exact"):
             out[k] = c.get(k)
         print(json.dumps(out), flush=True)
     sess.finish()
