@@ -33,6 +33,18 @@ static_assert(sizeof(NodeRec) == 64, "NodeRec must be one 64-byte line");
 
 constexpr uint32_t kLeafBit = 0x80000000u;
 
+// The tight box of a node: the bounding box of the target points below it, fp32 rounded outwards
+// (k_tight_boxes). The certified searches prune with it where the reference's own order does not
+// matter (a node's points all lie inside, so its squared box distance bounds every point's fl(d2)
+// from below, as the cell box does); cells are cubes, the points of a surface a thin slab: a far
+// query's ball dips into far fewer tight boxes than cells. One per NodeRec, 32 B.
+struct alignas(32) TBox {
+  float lo[3];
+  float hi[3];
+  float pad[2];
+};
+static_assert(sizeof(TBox) == 32, "TBox is 32 bytes");
+
 // Target point in leaf order (leaves in preorder, points in ascending original index —
 // the order the reference scans point_indices, octree.cpp:139).
 struct alignas(32) TgtPt {

@@ -99,6 +99,7 @@ static hipError_t reset_band(icp_hip_ctx* c) {
 
 static void free_target(icp_hip_ctx* c) {
   dfree(c->nodes);
+  dfree(c->tbox);
   dfree(c->pts);
   dfree(c->cells);
   c->cell_lmax = -1;
@@ -112,6 +113,7 @@ static NNLaunch base_launch(const icp_hip_ctx* c) {
   NNLaunch a;
   std::memset(&a, 0, sizeof(a));
   a.nodes = c->nodes;
+  a.tbox = c->tbox;
   a.pts = c->pts;
   a.counters = c->counters;
   a.n_nodes = (int32_t)c->n_nodes;
@@ -497,6 +499,8 @@ int icp_hip_set_target(icp_hip_ctx* c, const double* xyz, int64_t n, int max_poi
   if (c->cfg.certify_prev) HIP_TRY(launch_target_sep(c->nodes, c->pts, n, c->levels, c->stream));
   // after the separations (which a copy's flag overwrites: its separation is 0 either way)
   HIP_TRY(launch_mark_copies(c->pts, n, c->stream));
+  HIP_TRY(dalloc(&c->tbox, (size_t)c->n_nodes));
+  HIP_TRY(launch_tight_boxes(c->nodes, c->pts, c->tbox, c->n_nodes, c->max_depth, c->stream));
   // root box (host copy: the kernels' cell arithmetic starts from it) and the cell tables
   {
     NodeRec root;

@@ -91,6 +91,7 @@ struct icp_hip_ctx {
 
   // target (replicated on every rank)
   icp::NodeRec* nodes = nullptr;
+  icp::TBox* tbox = nullptr;  // tight boxes of the nodes (k_tight_boxes)
   icp::TgtPt* pts = nullptr;
   int64_t n_nodes = 0, n_leaves = 0, n_tgt = 0;
   int32_t pos0 = 0, max_depth = -1, levels = 1;

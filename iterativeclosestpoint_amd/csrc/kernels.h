@@ -74,6 +74,7 @@ static_assert(sizeof(WaveBox) == 64, "one line, eight words");
 struct NNLaunch {
   const LoopDev* loop;      // device loop (null: the host drives the iterate); T from loop->core.T
   const NodeRec* nodes;
+  const TBox* tbox;         // tight boxes of the nodes (prune tests of the certified searches)
   const TgtPt* pts;
   double* x;
   double* y;
@@ -130,6 +131,9 @@ hipError_t launch_nn(const NNLaunch& a, hipStream_t s);
 // TgtPt::sep of every target point (lower bound of its distance to every other point).
 hipError_t launch_target_sep(const NodeRec* nodes, TgtPt* pts, int64_t n, int levels, hipStream_t s);
 hipError_t launch_mark_copies(TgtPt* pts, int64_t n, hipStream_t s);
+// TBox of every node (icp_common.h), deepest level first; max_depth: the deepest node's depth.
+hipError_t launch_tight_boxes(const NodeRec* nodes, const TgtPt* pts, TBox* tb, int64_t n_nodes, int max_depth,
+                              hipStream_t s);
 
 struct CullLaunch {
   const LoopDev* loop;  // device loop: nothing to do once the session is done

@@ -688,18 +688,21 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
       nd.h12 = *reinterpret_cast<const double2*>(&nr->hi[1]);
       const int2 topo = *reinterpret_cast<const int2*>(&nr->first);
       const int32_t first = has ? topo.x : 0;
-      // the node itself against the current box (it met the box it was pushed against) and the
-      // group spheres: its squared box distance from a sphere's centre (rounding up to a few ulps,
-      // covered by the spheres' margin) at most the radius squared
-      bool live = has && nd.l01.x <= whx && nd.l2h0.y >= wlx && nd.l01.y <= why && nd.h12.x >= wly &&
-                  nd.l2h0.x <= whz && nd.h12.y >= wlz;
+      // the node's tight box (its points' bounding box; it was pushed by its cell) against the
+      // current box (it met the box it was pushed against) and the group spheres: its squared box
+      // distance from a sphere's centre (rounding up to a few ulps, covered by the spheres'
+      // margin) at most the radius squared
+      const float4 tb0 = *reinterpret_cast<const float4*>(&a.tbox[nid].lo[0]);
+      const float2 tb1 = *reinterpret_cast<const float2*>(&a.tbox[nid].hi[1]);
+      bool live = has && (double)tb0.x <= whx && (double)tb0.w >= wlx && (double)tb0.y <= why &&
+                  (double)tb1.x >= wly && (double)tb0.z <= whz && (double)tb1.y >= wlz;
       if (live) {
         bool any = false;
 #pragma unroll
         for (int g = 0; g < NG; g++)
           any = any || (sph_r2[g] > 0.0 &&  // 0: a group without joined lanes (its centre is not finite)
-                        !(box_s(nd.l01.x, nd.l01.y, nd.l2h0.x, nd.l2h0.y, nd.h12.x, nd.h12.y, sph_c[g][0],
-                                sph_c[g][1], sph_c[g][2]) > sph_r2[g]));
+                        !(box_s(tb0.x, tb0.y, tb0.z, tb0.w, tb1.x, tb1.y, sph_c[g][0], sph_c[g][1], sph_c[g][2]) >
+                          sph_r2[g]));
         live = any;
       }
       const uint32_t meta = live ? (uint32_t)topo.y : 0u;
@@ -1538,9 +1541,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8, 8))
 // area holds the walk's stack, the list and a staging area of its own (the stack stays live
 // through each segment's scan).
 constexpr int kWideLds = kWaveLds + 1024 + kWideQueue * 4;
-// (6 KB of LDS per wave admits ~6.5 waves per SIMD: compiled for 6, 80 VGPRs)
+// (8 KB of LDS per wave admits 5 waves per SIMD: compiled for 5, 96 VGPRs)
 #ifndef ICP_WIDE_WPE
-#define ICP_WIDE_WPE 6
+#define ICP_WIDE_WPE 5
 #endif
 template <int NG, bool DBG>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ICP_WIDE_WPE, ICP_WIDE_WPE))) k_nn_wide(NNLaunch a) {
@@ -1641,11 +1644,11 @@ constexpr int kBBPts = 256;     // kBBPts entries of which hold a step's leaf po
 // (a far query under a loose bound: every node within the bound is live) is searched again from
 // the root with the best point found so far as the bound, which prunes the frontier to the nodes
 // within the nearest distance (up to kBBPasses times while the bound shrinks). Returns false when
-// it still overflows (nothing written; the caller runs the reference-order DFS); otherwise writes
-// the certified result, or runs the reference-order DFS on lane 0 for a tie.
+// it still overflows and 2 for a tie (nothing written either way: the caller runs the
+// reference-order DFS), 1 after writing the certified result.
 constexpr int kBBPasses = 4;
-__device__ __forceinline__ bool wave_bb(const NNLaunch& a, int64_t i, double u, int32_t* stack,
-                                     unsigned long long* dfs_st, int lane) {
+constexpr int kBBDone = 1;
+__device__ __forceinline__ int wave_bb(const NNLaunch& a, int64_t i, double u, int32_t* stack, int lane) {
   const double qx = a.x[i], qy = a.y[i], qz = a.z[i];
   double best = __builtin_inf(), second = __builtin_inf();
   int32_t bpos = 0x7fffffff;
@@ -1678,13 +1681,12 @@ __device__ __forceinline__ bool wave_bb(const NNLaunch& a, int64_t i, double u, 
       const int32_t nid = has ? stack[tail - batch + lane] : 0;
       tail -= batch;
       const NodeRec* rr = a.nodes + nid;
-      const double2 l01 = *reinterpret_cast<const double2*>(&rr->lo[0]);
-      const double2 l2h0 = *reinterpret_cast<const double2*>(&rr->lo[2]);
-      const double2 h12 = *reinterpret_cast<const double2*>(&rr->hi[1]);
       const int2 topo = *reinterpret_cast<const int2*>(&rr->first);
       const uint32_t meta = (uint32_t)topo.y;
-      // pushed against an older (larger) bound: test the node itself again
-      const bool live = has && !(box_s(l01.x, l01.y, l2h0.x, l2h0.y, h12.x, h12.y, qx, qy, qz) > thr);
+      // pushed against an older (larger) bound, and pushed by its cell: test the node's tight box
+      const float4 tb0 = *reinterpret_cast<const float4*>(&a.tbox[nid].lo[0]);
+      const float2 tb1 = *reinterpret_cast<const float2*>(&a.tbox[nid].hi[1]);
+      const bool live = has && !(box_s(tb0.x, tb0.y, tb0.z, tb0.w, tb1.x, tb1.y, qx, qy, qz) > thr);
       const bool lf = live && (meta & kLeafBit);
       const uint32_t kids = (live && !lf) ? children_in_ball(rr, meta & 0xffu, qx, qy, qz, thr) : 0u;
       // The step's leaf points, flat: listed in LDS kBBPts at a time and scanned kBBPts / 64 per
@@ -1762,24 +1764,19 @@ __device__ __forceinline__ bool wave_bb(const NNLaunch& a, int64_t i, double u, 
     atomicAdd(&a.dbg[28], (unsigned long long)steps);
     if (over) atomicAdd(&a.dbg[37], 1ull);
   }
-  if (over) return false;
+  if (over) return 0;
   // the wave's best, and its second: the smallest of the other lanes' bests and the best lane's
   // second (a best held by two lanes is its own second: a tie)
   const double gb = wave_min_d(best);
   const unsigned long long at = __ballot(best == gb);
   const double gs = __popcll(at) > 1 ? gb : wave_min_d(best == gb ? second : best);
   const int32_t gp = (int32_t)__builtin_amdgcn_readlane(bpos, __builtin_ctzll(at ? at : 1ull));
-  if (certified(gb, gs, a.init_best)) {
-    if (lane == 0) {
-      a.pos_out[i] = gp;
-      a.dist_out[i] = __builtin_sqrt(gb);
-    }
-  } else if (lane == 0) {
-    exact_query(a, i, dfs_st, 1);
-    atomicAdd(a.fb_count + 3, 1u);  // a DFS finish of the ball search (icp_iter_stats.n_fallback)
-    if (a.dbg) atomicAdd(&a.dbg[38], 1ull);
+  if (!certified(gb, gs, a.init_best)) return 2;
+  if (lane == 0) {
+    a.pos_out[i] = gp;
+    a.dist_out[i] = __builtin_sqrt(gb);
   }
-  return true;
+  return kBBDone;
 }
 
 __global__ void __launch_bounds__(64) k_nn_ball(NNLaunch a) {
@@ -1830,7 +1827,9 @@ __global__ void __launch_bounds__(64) k_nn_ball(NNLaunch a) {
       const int64_t iq = __builtin_amdgcn_readlane(e, k) & 0x3fffffff;
       const double uq = readlane_d(qu, k);
       // the stack in the DFS columns' area (free now); the fallback DFS after it, in the same area
-      if (!wave_bb(a, iq, uq, reinterpret_cast<int32_t*>(lds_raw), lds_raw, lane) && lane == 0) {
+      // the stack in the DFS columns' area (free now); a tie or an overflow: the reference-order
+      // DFS on lane 0, in the same area
+      if (wave_bb(a, iq, uq, reinterpret_cast<int32_t*>(lds_raw), lane) != kBBDone && lane == 0) {
         exact_query(a, iq, lds_raw, 1);
         atomicAdd(a.fb_count + 3, 1u);
         if (a.dbg) atomicAdd(&a.dbg[38], 1ull);
@@ -1852,17 +1851,32 @@ __global__ void __launch_bounds__(64) k_nn_ball(NNLaunch a) {
   // 4's window 4 % (its 15k-query lists of easy balls).
   // (icp_hip_config.ball_mode: 0 this rule, 1 the ball walk always, 2 direct always)
   if (a.ball_mode == 2 || (a.ball_mode == 0 && (cnt <= gridDim.x || cnt > 4u * gridDim.x))) {
+    // A query the cooperative search leaves (a tie, an overflow) is queued for the reference-order
+    // DFS; the queue runs 64 at a time, one per lane, each with its DFS stack column in LDS (ties
+    // come in numbers where both clouds sit on the LAS grid: the source's first iterate)
     unsigned taken = 0;
+    int dq = 0;  // wave-uniform
+    auto dfs_flush = [&]() {
+      wave_lds_fence();
+      if (lane < dq) exact_query(a, fq[lane], lds_raw + lane, 64);
+      if (lane == 0) {
+        atomicAdd(a.fb_count + 3, (unsigned)dq);
+        if (a.dbg) atomicAdd(&a.dbg[38], (unsigned long long)dq);
+      }
+      dq = 0;
+      wave_lds_fence();
+    };
     for (unsigned j = blockIdx.x; j < cnt; j += gridDim.x, ++taken) {
       const int64_t i = a.fb_list2[j];
       const double u = a.fb_u2[j];
-      if (!wave_bb(a, i, u, reinterpret_cast<int32_t*>(lds_raw), lds_raw, lane) && lane == 0) {
-        exact_query(a, i, lds_raw, 1);
-        atomicAdd(a.fb_count + 3, 1u);
-        if (a.dbg) atomicAdd(&a.dbg[38], 1ull);
+      if (wave_bb(a, i, u, reinterpret_cast<int32_t*>(lds_raw), lane) != kBBDone) {
+        wave_lds_fence();
+        if (lane == 0) fq[dq] = (int32_t)i;
+        if (++dq == 64) dfs_flush();
       }
       wave_lds_fence();
     }
+    if (dq > 0) dfs_flush();
     // the queries taken by the cooperative search count as follow-up searches, as after the ball
     // walk (icp_iter_stats.n_lane_search)
     if (lane == 0 && taken > 0) atomicAdd(a.fb_count + 2, taken);

@@ -78,9 +78,76 @@ __global__ void k_mark_copies(TgtPt* pts, int64_t n) {
   if (copy) pts[j].sep = -0.0f;  // a copy's separation is 0 (certify_prev): the sign is the flag
 }
 
+// v rounded down / up to fp32 (finite v; the conversion rounds to nearest, then one ulp outwards
+// when it went the wrong way)
+__device__ __forceinline__ float f32_step(float f, bool up) {
+  if (f == 0.f) return up ? 0x1p-149f : -0x1p-149f;
+  const int b = __float_as_int(f);
+  return __int_as_float((f > 0.f) == up ? b + 1 : b - 1);
+}
+__device__ __forceinline__ float f32_down(double v) {
+  const float f = (float)v;
+  return (double)f > v ? f32_step(f, false) : f;
+}
+__device__ __forceinline__ float f32_up(double v) {
+  const float f = (float)v;
+  return (double)f < v ? f32_step(f, true) : f;
+}
+
+// Tight boxes of the nodes at one depth (deepest first): a leaf's from its points, an inner node's
+// the union of its children's (one level deeper, done by the previous launch).
+__global__ void k_tight_boxes(const NodeRec* nodes, const TgtPt* pts, TBox* tb, int64_t n_nodes, int depth) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n_nodes) return;
+  const NodeRec& nd = nodes[j];
+  if (nd.depth != depth) return;
+  TBox b;
+  if (nd.meta & kLeafBit) {
+    double lo[3] = {__builtin_inf(), __builtin_inf(), __builtin_inf()};
+    double hi[3] = {-__builtin_inf(), -__builtin_inf(), -__builtin_inf()};
+    const int32_t cnt = (int32_t)(nd.meta & ~kLeafBit);
+    for (int32_t k = 0; k < cnt; k++) {
+      const TgtPt& p = pts[nd.first + k];
+      lo[0] = p.x < lo[0] ? p.x : lo[0];
+      lo[1] = p.y < lo[1] ? p.y : lo[1];
+      lo[2] = p.z < lo[2] ? p.z : lo[2];
+      hi[0] = p.x > hi[0] ? p.x : hi[0];
+      hi[1] = p.y > hi[1] ? p.y : hi[1];
+      hi[2] = p.z > hi[2] ? p.z : hi[2];
+    }
+    for (int k = 0; k < 3; k++) {
+      b.lo[k] = cnt > 0 ? f32_down(lo[k]) : __builtin_inff();  // an empty leaf: an empty box
+      b.hi[k] = cnt > 0 ? f32_up(hi[k]) : -__builtin_inff();
+    }
+  } else {
+    for (int k = 0; k < 3; k++) {
+      b.lo[k] = __builtin_inff();
+      b.hi[k] = -__builtin_inff();
+    }
+    const int nk = __builtin_popcount(nd.meta & 0xffu);
+    for (int c = 0; c < nk; c++) {
+      const TBox& cb = tb[nd.first + c];
+      for (int k = 0; k < 3; k++) {
+        b.lo[k] = cb.lo[k] < b.lo[k] ? cb.lo[k] : b.lo[k];
+        b.hi[k] = cb.hi[k] > b.hi[k] ? cb.hi[k] : b.hi[k];
+      }
+    }
+  }
+  b.pad[0] = b.pad[1] = 0.f;
+  tb[j] = b;
+}
+
 inline unsigned grid_for(int64_t n, int bs) { return (unsigned)((n + bs - 1) / bs); }
 
 }  // namespace
+
+hipError_t launch_tight_boxes(const NodeRec* nodes, const TgtPt* pts, TBox* tb, int64_t n_nodes, int max_depth,
+                              hipStream_t s) {
+  if (n_nodes <= 0) return hipSuccess;
+  for (int d = max_depth; d >= 0; d--)
+    hipLaunchKernelGGL(k_tight_boxes, dim3(grid_for(n_nodes, 256)), dim3(256), 0, s, nodes, pts, tb, n_nodes, d);
+  return hipGetLastError();
+}
 
 hipError_t launch_mark_copies(TgtPt* pts, int64_t n, hipStream_t s) {
   if (n <= 0) return hipSuccess;

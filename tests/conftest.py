@@ -36,6 +36,12 @@ def golden_engine():
 
 
 @pytest.fixture(scope="session")
+def golden_scene():
+    """A LiDAR-like surface pair run through the reference (gen_golden.py scene_cases)."""
+    return np.load(GOLDEN / "scene_ref.npz")
+
+
+@pytest.fixture(scope="session")
 def golden_core_las():
     return np.load(GOLDEN / "core_las.npz")
 

@@ -10,7 +10,7 @@ Eigen 3.3.4, built by oracle/Makefile (`make -C oracle ref`), and oracle/_ref/li
 deterministic generator (icp_synth_pair) or from numpy with fixed seeds, and are stored
 alongside (or as hashes, for the 100k case).
 
-Run from the repo root:  python tests/golden/gen_golden.py [--only-engine | --only-las]
+Run from the repo root:  python tests/golden/gen_golden.py [--only-engine | --only-las | --only-scene]
 """
 from __future__ import annotations
 
@@ -353,9 +353,60 @@ def core_las():
     return {"n": n, "file_bytes": len(blob), "file_fnv1a": fnv1a(arrays["core_file"])}
 
 
+def scene_cases():
+    """A LiDAR-like surface pair (icp_synth_scene on a 3 m site: ground + walls from two scanner
+    poses, ~1 cm spacing, 1 mm LAS grid, occlusion shadows, the blind disc under the scanner,
+    0.2 % outliers) through the reference: the CLI octree's correspondences of the source as given
+    and of the source the CLI ICP leaves (icp_registration.cpp:107-205, init 1e20), the CLI ICP's
+    per-iteration cumulative transforms (:443-622), and the core engine's registration
+    (core/icpengine.cpp)."""
+    n, site = 30000, 3.0
+    tgt, src, Ttrue = icp.synth_scene(n, site_radius=site)
+    arrays = {"scene_target": tgt, "scene_source": src, "scene_T_true": Ttrue}
+    ref = O.reference()
+
+    def ref_dist(q, t, idx):
+        return np.array([ref.ref_distance(np.ascontiguousarray(q[i]).ctypes.data_as(O.C.c_void_p),
+                                          np.ascontiguousarray(t[idx[i]]).ctypes.data_as(O.C.c_void_p))
+                         for i in range(len(q))])
+
+    tree = O.RefTree(tgt)
+    idx0 = tree.nn(src)
+    arrays["scene_idx_iter0_cli"] = idx0
+    arrays["scene_dist_iter0_cli"] = ref_dist(src, tgt, idx0)
+    iters, tol = 20, 1e-9
+    R, tt, tcums, src_out = O.ref_icp_cli(src, tgt, iters, tol)
+    arrays["scene_cli_R_final"] = R
+    arrays["scene_cli_t_final"] = tt
+    arrays["scene_cli_T_cums"] = tcums
+    arrays["scene_cli_source_out"] = src_out
+    idxf = tree.nn(src_out)
+    arrays["scene_idx_final_cli"] = idxf
+    arrays["scene_dist_final_cli"] = ref_dist(src_out, tgt, idxf)
+    eng = {"iterations": 10, "tolerance": 0.0, "sigma": 3.0}
+    r = O.ref_engine_register(src, tgt, eng["iterations"], eng["tolerance"], eng["sigma"])
+    arrays["scene_engine_history"] = r["history"]
+    arrays["scene_engine_R"] = r["final_R"]
+    arrays["scene_engine_t"] = r["final_t"]
+    arrays["scene_engine_source_out"] = r["source_out"]
+    np.savez_compressed(OUT / "scene_ref.npz", **arrays)
+    q = np.round(tgt * 1000).astype(np.int64)
+    return {"n": n, "site_radius": site, "cli_iterations": iters, "cli_tolerance": tol,
+            "n_transforms": int(len(tcums)), "target_copies": int(n - len(np.unique(q, axis=0))),
+            "engine": dict(eng, finished=r["finished"], total_iterations=r["total_iterations"],
+                           final_rmse=r["final_rmse"], message=r["message"]),
+            "inputs": "icp_synth_scene(30000, site_radius=3.0), stored in scene_ref.npz"}
+
+
 def main():
     if not O.reference_available():
         O.build(ref=True)
+    if "--only-scene" in sys.argv:
+        meta = json.loads((OUT / "golden.json").read_text())
+        meta["scene_ref"] = scene_cases()
+        (OUT / "golden.json").write_text(json.dumps(meta, indent=1, sort_keys=True))
+        print(json.dumps(meta["scene_ref"], indent=1))
+        return
     if "--only-engine" in sys.argv:
         meta = json.loads((OUT / "golden.json").read_text())
         meta["engine_rules"] = engine_cases()
@@ -381,6 +432,7 @@ def main():
     meta["las_report"] = las_and_report()
     meta["engine_rules"] = engine_cases()
     meta["core_las"] = core_las()
+    meta["scene_ref"] = scene_cases()
     meta["engine_reference"] = ("PointCloudRegistration/core/{icpengine,octree,pointcloud,lasio}.cpp + moc, "
                                 "Qt 5.9.7 (/opt/conda), g++ -O2 -ffp-contract=off, no -march "
                                 "(oracle/_ref/libicp_ref_engine.so)")

@@ -326,3 +326,34 @@ def test_device_loop_batch_longer_than_deadline(icp):
         wall_ms = (time.perf_counter() - t0) * 1e3
         assert wall_ms > 2 * 8, wall_ms  # the batch really outlasted the per-iterate deadline
         s.close()
+
+
+def test_comm_info_and_exchange_timings(icp, pair):
+    """What a launcher can verify about the exchange: RCCL's own view of the communicator
+    (ncclCommCount / ncclCommUserRank / ncclCommCuDevice through icp_hip_comm_info) and the time
+    of the two record all-gathers of each timed iterate (icp_hip_exchange_timings)."""
+    tgt, src = pair
+    with icp.Context(0, icp.config(timing_stride=1)) as ctx:
+        assert ctx.comm_info() == {"count": 1, "rank": 0, "device": 0, "transport": icp.XPORT_AUTO}
+        ctx.set_target(tgt, 10, 20, icp.RULES_ENGINE)
+        ctx.set_source(src)
+        ctx.iterate(None, 0, icp.RULES_ENGINE, 3.0)
+        assert np.isnan(ctx.exchange_timings(1)).all()  # no peers: no exchange
+        ctx.comm_init(1, 0, icp.Context.unique_id())
+        assert ctx.comm_info() == {"count": 1, "rank": 0, "device": 0, "transport": icp.XPORT_RCCL}
+        for it in range(3):
+            ctx.iterate(None, it, icp.RULES_ENGINE, 3.0)
+        x = ctx.exchange_timings(3)
+        assert np.isfinite(x).all() and (x > 0).all() and (x < 50).all(), x
+        # the host exchange: the callback's world, timed by the host clock
+        ctx.comm_init_host(2, 1, lambda local: np.stack([local, local]))
+        assert ctx.comm_info() == {"count": 2, "rank": 1, "device": 0, "transport": icp.XPORT_CALLBACK}
+        ctx.set_source(src)
+        ctx.iterate(None, 0, icp.RULES_ENGINE, 3.0)
+        assert np.isfinite(ctx.exchange_timings(1)).all()
+    with icp.Context(devices=[0, 0, 0]) as g:  # an in-process group (host gather) of three members
+        for m in range(3):
+            info = g.comm_info(m)
+            assert info["count"] == 3 and info["rank"] == m and info["device"] == 0
+        with pytest.raises(icp.IcpError):
+            g.comm_info(3)

@@ -132,3 +132,42 @@ def test_wide_pass_modes_agree(icp, oracle, scene, which):
         for (i0, d0), (i1, d1) in zip(out[key][1], out[(1, 1)][1]):
             np.testing.assert_array_equal(i0, i1)
             np.testing.assert_array_equal(d0, d1)
+
+
+def test_scene_vs_reference_fixture(icp, golden_scene, golden_meta):
+    """The HIP path on the REFERENCE's own surface fixture (tests/golden/scene_ref.npz, made by
+    oracle/_ref from icp_registration.cpp and core/icpengine.cpp): the CLI octree's correspondences
+    and residuals of the source and of the CLI ICP's final source bit for bit; the CLI ICP's 20
+    cumulative transforms; the core engine's 10-iterate registration (north star: 1e-6 RMSE;
+    asserted to 1e-9)."""
+    g, m = golden_scene, golden_meta["scene_ref"]
+    src, tgt = g["scene_source"], g["scene_target"]
+    with icp.Context(0) as ctx:
+        ctx.set_target(tgt, 10, 20, icp.RULES_CLI)
+        for q, key in ((src, "iter0"), (g["scene_cli_source_out"], "final")):
+            idx, d = ctx.nn(q)
+            np.testing.assert_array_equal(idx, g[f"scene_idx_{key}_cli"], err_msg=key)
+            np.testing.assert_array_equal(d, g[f"scene_dist_{key}_cli"], err_msg=key)
+    R, t, tcums, out = icp.cli_icp(src, tgt, m["cli_iterations"], m["cli_tolerance"], device=0)
+    ref = g["scene_cli_T_cums"]
+    assert tcums.shape == ref.shape
+    assert _trmse(tcums[-1], ref[-1]) < 1e-6
+    np.testing.assert_allclose(tcums, ref, atol=1e-9)
+    np.testing.assert_allclose(out, g["scene_cli_source_out"], atol=1e-8)
+    e = m["engine"]
+    p = icp.params_default(max_iterations=e["iterations"], tolerance=e["tolerance"], sigma_multiplier=e["sigma"])
+    rc, res, hist, out = icp.engine_register(p, src, tgt, device=0)
+    assert rc == 0 and res.success and res.total_iterations == e["total_iterations"]
+    Tg, Tr = _Tres(res), np.eye(4)
+    Tr[:3, :3] = g["scene_engine_R"]
+    Tr[:3, 3] = g["scene_engine_t"]
+    assert _trmse(Tg, Tr) < 1e-6
+    np.testing.assert_allclose(Tg, Tr, atol=1e-9)
+    np.testing.assert_allclose(res.final_rmse, e["final_rmse"], rtol=1e-9)
+    np.testing.assert_allclose(out, g["scene_engine_source_out"], atol=1e-8)
+    h = g["scene_engine_history"]
+    assert [r.valid_points for r in hist] == [int(x) for x in h[: len(hist), 2]]
+
+
+def _trmse(a, b):
+    return float(np.sqrt(np.mean((np.asarray(a) - np.asarray(b)) ** 2)))
