@@ -100,7 +100,9 @@ typedef struct icp_hip_config {
   int32_t overflow_halves; /* 1: in the first iterate of a source (descent guesses, ~16 % of
                               the waves overflow), the queries of a wave whose search box
                               overflows are searched again as two 32-query halves (k_nn_half)
-                              before the ball search; 0: they go to the ball search     dflt 1 */
+                              before the wide pass / ball search; 0: the wide pass takes the
+                              whole wave (wide_pass; measured better on the blob and the
+                              scene: first iterate 2.45 -> 2.38 ms, 41 -> 29.6 ms)   dflt 0 */
   int32_t device_loop;    /* 1: the engine session's batches (icp_session_step_n, icp_engine_run)
                              run as a device-resident loop: each iteration's last kernel takes
                              the session's decisions and computes the transform (the host

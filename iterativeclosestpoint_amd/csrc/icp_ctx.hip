@@ -201,7 +201,7 @@ void icp_hip_config_default(icp_hip_config* cfg) {
   cfg->candidate_loose = 190;
   cfg->candidate_lead = 8;
   cfg->fused_cull = 1;
-  cfg->overflow_halves = 1;
+  cfg->overflow_halves = 0;
   cfg->device_loop = 0;
   cfg->timing_stride = 0;
   cfg->peer_timeout_ms = 0;

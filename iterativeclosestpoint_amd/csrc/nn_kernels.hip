@@ -101,6 +101,10 @@ __global__ void __launch_bounds__(256) k_nn_ref(NNLaunch a) {
 // the certificate of nn_device.h applies. Non-joined lanes go to the ball list, uncertified ones
 // to the exact list.
 constexpr int kOpenToBall = 4;   // certify_prev 3: open queries a wave hands to the ball search
+constexpr int kMaxTableLevels = 9;  // cell tables are built for levels 0..9 at most (octree_gpu.hip)
+#ifndef ICP_TABLE_DESCENT
+#define ICP_TABLE_DESCENT 1  // a source's first-iterate descent starts from the cell tables
+#endif
 constexpr int kWaveQueue = 256;  // node ids of the walk's LIFO stack (staging area after the walk)
 constexpr int kWaveStartK = 2;   // start cells per lane (up to 128 start nodes per wave)
 constexpr int kWavePoints = 1024;  // candidate list area (up to kWaveCandCap ids)
@@ -108,9 +112,15 @@ static_assert(kWaveCandCap <= kWavePoints, "candidate list");
 constexpr int kWaveLds = kWaveQueue * 4 + kWavePoints * 4;  // 5 KB per wave
 constexpr int kWideQueue = 512;  // the wide pass's node stack (after its staging area)
 #ifndef ICP_WIDE_SEGS
-#define ICP_WIDE_SEGS 6
+#define ICP_WIDE_SEGS 2
 #endif
-constexpr int kWideSegs = ICP_WIDE_SEGS;  // segments a wide walk scans before it gives up
+#ifndef ICP_WIDE_SEGS0
+#define ICP_WIDE_SEGS0 6
+#endif
+// segments a wide walk scans before it gives up: after a search (the bounds are the previous
+// matches' distances, tight), and in a source's first iterate (descent guesses, which the first
+// segments tighten)
+constexpr int kWideSegs = ICP_WIDE_SEGS, kWideSegs0 = ICP_WIDE_SEGS0;
 static_assert(kWaveQueue * 4 >= 64 * 16 && kWaveQueue * 4 >= 32 * 32, "staging area aliases the stack");
 static_assert(kWaveQueue * 4 + kWavePoints * 4 >= 128 * 16, "a reusing wave stages 128 points (stack + list area)");
 
@@ -301,9 +311,26 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
     u = dx * dx + dy * dy + dz * dz;
     if (CERT) safe = prev_certified(u, pp->sep, a.init_best);
   } else if (active && finite_q) {
-    const NodeRec* r0 = a.nodes;
-    double lx = r0->lo[0], ly = r0->lo[1], lz = r0->lo[2], hx = r0->hi[0], hy = r0->hi[1], hz = r0->hi[2];
     int32_t node = 0;
+    if (ICP_TABLE_DESCENT && a.cells && a.cell_lmax > 0) {
+      // The descent's first levels from the cell tables: the query's cell path at the deepest
+      // table level (the octree's own midpoint comparisons), then the deepest level whose cell
+      // holds points (every level's entry read at once). Any start gives a valid guess; this one
+      // is the node the descent from the root would pass through when the query's cells exist.
+      const int L = a.cell_lmax;
+      const uint32_t px = axis_path(qx, a.root_lo[0], a.root_hi[0], L);
+      const uint32_t py = axis_path(qy, a.root_lo[1], a.root_hi[1], L);
+      const uint32_t pz = axis_path(qz, a.root_lo[2], a.root_hi[2], L);
+      const uint32_t key = spread3(px) | (spread3(py) << 1) | (spread3(pz) << 2);
+      int32_t e[kMaxTableLevels];
+#pragma unroll
+      for (int l = 1; l <= kMaxTableLevels; l++)
+        e[l - 1] = l <= L ? a.cells[((((int64_t)1 << (3 * l)) - 1) / 7) + (key >> (3 * (L - l)))] : -1;
+#pragma unroll
+      for (int l = 1; l <= kMaxTableLevels; l++) node = e[l - 1] >= 0 ? (e[l - 1] >> 5) : node;
+    }
+    const NodeRec* r0 = a.nodes + node;
+    double lx = r0->lo[0], ly = r0->lo[1], lz = r0->lo[2], hx = r0->hi[0], hy = r0->hi[1], hz = r0->hi[2];
     int32_t pfirst = -1;  // the current node's parent: its first child record, child mask, the
     uint32_t pmask = 0, po = 0;  // octant taken and its children's squared axis distances
     double psx[2] = {0.0, 0.0}, psy[2] = {0.0, 0.0}, psz[2] = {0.0, 0.0};
@@ -746,7 +773,7 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
         wave_lds_fence();  // the segment's reads of the list are done before it is refilled
         // a box this dense for its balls (their bounding box cuts a surface far wider than the
         // balls do) is left to the per-query searches, with the bounds found so far
-        if (segs >= kWideSegs && tail > 0) {
+        if (segs >= (have_prev ? kWideSegs : kWideSegs0) && tail > 0) {
           if (kDbg && a.dbg && lane == 0) atomicAdd(&a.dbg[34], 1ull);
           return false;
         }

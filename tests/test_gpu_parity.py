@@ -263,7 +263,8 @@ def test_fallback_share_small_on_scans(icp, gpu_ctx):
                                    (300_000, {"xcd_blocks": 0}),
                                    (1_000_000, {"candidate_cache": 0}), (300_000, {"candidate_margin": 0}),
                                    (300_000, {"candidate_margin": 256}),
-                                   (1_000_000, {"overflow_halves": 0}), (1_000_000, {"certify_prev": 3}),
+                                   (1_000_000, {"overflow_halves": 1}), (1_000_000, {"wide_pass": 1}),
+                                   (1_000_000, {"wide_pass": 2}), (1_000_000, {"certify_prev": 3}),
                                    (300_000, {"certify_prev": 2, "candidate_cache": 0})])
 def test_scan32_matches_fp64_scan(icp, n, cfg):
     """Every configuration of the certified search (fp32 filter scan vs fp64 scan, cell-table
@@ -435,7 +436,7 @@ def test_overflowing_waves_take_the_half_pass(icp, oracle):
     at 1M: ~16 % of the waves) is searched again as two 32-query halves with their own smaller
     boxes (k_nn_half) before anything goes to the ball search; every result stays the reference's."""
     tgt, src, _ = icp.synth_pair(1_000_000)
-    with icp.Context(0, {"debug_counters": 1}) as ctx:
+    with icp.Context(0, {"debug_counters": 1, "overflow_halves": 1}) as ctx:
         ctx.set_target(tgt, 10, 20, icp.RULES_ENGINE)
         ctx.set_source(src)
         st = ctx.iterate(None, 0, icp.RULES_ENGINE, 3.0)
@@ -447,6 +448,25 @@ def test_overflowing_waves_take_the_half_pass(icp, oracle):
     np.testing.assert_array_equal(d, od)
     # the halves took most of the overflowed queries off the ball search
     assert st.n_ball_search < 64 * c["overflow_waves"], (st.n_ball_search, c)
+
+
+def test_overflowing_waves_take_the_wide_pass(icp, oracle):
+    """By default (overflow_halves 0, wide_pass 0) a wave whose box overflows its candidate list
+    in the first iterate is searched again by the wide pass (k_nn_wide: the same 64 lanes, the box
+    walked and scanned in segments, bounds tightened after each); the results stay the reference's
+    and most overflowed queries never reach the ball search."""
+    tgt, src, _ = icp.synth_pair(1_000_000)
+    with icp.Context(0, {"debug_counters": 1}) as ctx:
+        ctx.set_target(tgt, 10, 20, icp.RULES_ENGINE)
+        ctx.set_source(src)
+        st = ctx.iterate(None, 0, icp.RULES_ENGINE, 3.0)
+        c = ctx.debug_counters()
+        idx, d = ctx.get_correspondences()
+    assert c["overflow_waves"] > 0 and c["wide_waves"] == c["overflow_waves"] and c["halves"] == 0, c
+    oidx, od = oracle.OracleTree(tgt).nn(src, init_best=oracle.DBL_MAX)
+    np.testing.assert_array_equal(idx, oidx)
+    np.testing.assert_array_equal(d, od)
+    assert st.n_ball_search < 16 * c["overflow_waves"], (st.n_ball_search, c)
 
 
 def test_host_and_device_query_orders(icp, oracle):

@@ -2,7 +2,9 @@
 """Per-phase clocks and counters of the wave search on the bench workload (diagnostic build of
 the library with -DICP_PHASE_CLOCKS=1 loaded through ICP_HIP_LIB; debug counters enabled).
 
-usage: ICP_HIP_LIB=iterativeclosestpoint_amd/libicp_hip_clk.so python3 tools/phase_probe.py [N]
+usage: ICP_HIP_LIB=iterativeclosestpoint_amd/libicp_hip_clk.so python3 tools/phase_probe.py [N] [first]
+  first: the phases of a source's first iterate (descent guesses, every wave walks) instead of a
+  steady one
 """
 import sys
 from pathlib import Path
@@ -17,10 +19,13 @@ tgt, src, _ = icp.synth_pair(n)
 with icp.Context(0, icp.config(debug_counters=1, timing_stride=1)) as ctx:
     ctx.set_target(tgt, 10, 20, icp.RULES_ENGINE)
     ctx.set_source(src)
-    sess = ctx.session(icp.params_default(max_iterations=20, tolerance=1e-6, flags=icp.FLAG_NO_EARLY_STOP))
-    for _ in range(6):
-        sess.step()
-    st = ctx.iterate(None, 1, icp.RULES_ENGINE, 3.0)
+    if len(sys.argv) > 2 and sys.argv[2] == "first":
+        st = ctx.iterate(None, 0, icp.RULES_ENGINE, 3.0)
+    else:
+        sess = ctx.session(icp.params_default(max_iterations=20, tolerance=1e-6, flags=icp.FLAG_NO_EARLY_STOP))
+        for _ in range(6):
+            sess.step()
+        st = ctx.iterate(None, 1, icp.RULES_ENGINE, 3.0)
     import ctypes as C
     out = np.zeros(icp._lib.DBG_SLOTS, np.uint64)
     icp._lib._check(icp.lib().icp_hip_debug_counters(ctx.handle, icp._lib._ptr(out)))
