@@ -281,11 +281,12 @@ def test_host_exchange_deadline(icp, pair):
 
 def test_rccl_deadline_aborts_and_recovers(icp):
     """config.peer_timeout_ms over an RCCL communicator: an iterate that outlasts it (a 1 ms
-    deadline on the first iterate of a 5M source, ~2 ms of device time) is abandoned with
-    ncclCommAbort and ERCCL in bounded time; comm_init restores the multi-rank path."""
+    deadline on an iterate of a 5M source with the reference-order search: tens of ms of device
+    time, so the deadline is certain to pass whatever the certified search's speed) is abandoned
+    with ncclCommAbort and ERCCL in bounded time; comm_init restores the multi-rank path."""
     import time
     tgt, src, _ = icp.synth_pair(5_000_000)
-    with icp.Context(0, icp.config(peer_timeout_ms=1)) as ctx:
+    with icp.Context(0, icp.config(peer_timeout_ms=1, search=icp.SEARCH_REFERENCE)) as ctx:
         ctx.set_target(tgt, 10, 20, icp.RULES_ENGINE)
         ctx.set_source(src)
         ctx.synchronize()
