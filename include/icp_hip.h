@@ -162,8 +162,9 @@ typedef struct icp_hip_config {
                               convergence, occlusion shadows): 0 (auto) searched again by the wide
                               pass (k_nn_wide: the same box walked and scanned in segments by the
                               same 64 lanes) in a source's first iterate and whenever the previous
-                              iterate had >= 256 such waves, else their queries take the ball
-                              search; 1 never; 2 always. The same results either way     dflt 0 */
+                              iterate had >= max(256, waves / 32) such waves, else their queries
+                              take the ball search; 1 never; 2 always. The same results either
+                              way                                                          dflt 0 */
   int32_t reserved[3];     /* zero (fields of later versions of this header); create_ex rejects
                               a nonzero word                                                    */
 } icp_hip_config;

@@ -711,12 +711,20 @@ static int wait_device(icp_hip_ctx* c, Done done, Progress progress, const char*
 static int32_t* wide_list(int32_t* fbl, int64_t n) { return fbl + 2 * n + n / 16 + 8; }
 
 // config.wide_pass: 0 a source's first iterate (descent guesses: loose boxes) and any iterate after
-// one with >= kWideAuto overflowing waves (surface data far from convergence, occlusion shadows;
-// the ball search takes the queries of a few hundred waves sooner than a second launch); 2 always
+// one with >= max(kWideAuto, waves / kWideAutoDiv) overflowing waves (surface data far from
+// convergence); below that the ball search takes their queries sooner than a second launch (the
+// blob's ~300 overflowing waves at 10M: a 100 us wide launch; profiles/r22/ab/ab_wide_auto.txt:
+// 10M scene window +4.6 %, blob window +2.5 % against the fixed 256); 2 always
 static constexpr double kWideAuto = 256.0;
+#ifndef ICP_WIDE_AUTO_DIV
+#define ICP_WIDE_AUTO_DIV 32
+#endif
+static constexpr double kWideAutoDiv = ICP_WIDE_AUTO_DIV;
 static bool wide_pass_on(const icp_hip_ctx* c) {
   if (!c->cfg.scan32 || c->cfg.search != ICP_SEARCH_CERTIFIED || c->cfg.wide_pass == 1) return false;
-  return c->cfg.wide_pass == 2 || !c->have_prev || c->last_wide >= kWideAuto;
+  const double rel = (double)((c->n_src + 63) / 64) / kWideAutoDiv;
+  const double thr = rel > kWideAuto ? rel : kWideAuto;
+  return c->cfg.wide_pass == 2 || !c->have_prev || c->last_wide >= thr;
 }
 
 // One iterate enqueued on the context's stream, no wait. Host-driven (loop_slot < 0): the

@@ -36,6 +36,23 @@ constexpr bool kDbgCounts = !ICP_PHASE_CLOCKS;  // the clock build counts nothin
 #else
 #define PCLK(v)
 #endif
+// Diagnostic build only (-DICP_PHASE_STOP=1): the wave search returns after the phase set by
+// icp_hip_debug_phase_stop (1: the first round trip, 2: the guess, 3: the box, 4: the walk, 5: the
+// scan and the winner's fp64 distance, 6: certify, write and queue; 0: none), so SQ counters of one
+// launch per setting give the instructions of each phase (tools/phase_insts.py). The results of
+// such a launch are not the search's: it is for counting only.
+#ifndef ICP_PHASE_STOP
+#define ICP_PHASE_STOP 0
+#endif
+#if ICP_PHASE_STOP
+namespace icp {
+__device__ int g_phase_stop;
+}
+#define PSTOP(k) \
+  if (__builtin_amdgcn_readfirstlane(icp::g_phase_stop) == (k)) return
+#else
+#define PSTOP(k)
+#endif
 namespace icp {
 
 namespace {
@@ -298,6 +315,7 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
   const bool finite_q = __builtin_isfinite(qx) && __builtin_isfinite(qy) && __builtin_isfinite(qz);
 
   PCLK(t_p0);
+  PSTOP(1);
   // Phase 1: the guess (any value is safe: certification also requires best <= u).
   double u = __builtin_inf();
   int32_t gpos = -1;  // (first iterate) the target point whose distance is u
@@ -478,6 +496,7 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
   }
 
   PCLK(t_p1);
+  PSTOP(2);
   // Phase 2: the wave's search box over the lanes that join. Every point with fl(d2) <= u (1 +
   // 2^-47) lies within r of the query, r >= sqrt(u) (1 + 2^-40) + |q|_max 2^-45 (ball_radius32).
   const double amax = __builtin_fmax(__builtin_fabs(qx), __builtin_fmax(__builtin_fabs(qy), __builtin_fabs(qz)));
@@ -590,6 +609,7 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
   if (have_rec) group_bounds(pext * 0x1p-20f);
 
   PCLK(t_p2);
+  PSTOP(3);
   // Phase 3: the leaves meeting B. With the candidate cache (iterate only), a walk collects the
   // leaves meeting B+ = B enlarged by wc_margin x its largest half-extent per side and stores the
   // points inside B+ (as the scan stages them: fp32 offsets from B+'s centre, and the id); the
@@ -1000,6 +1020,7 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
   }
 
   PCLK(t_p3);
+  PSTOP(4);
   // Phase 4: the lockstep scan: 64 candidates per chunk, the next chunk's loads in flight while
   // the current one is scanned from LDS (a reusing wave streams its cache entries; a walking wave
   // gathers the points of its list and, with the cache, stores those inside B+).
@@ -1462,6 +1483,7 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
   }
 
   PCLK(t_p4);
+  PSTOP(5);
   // Phase 5: certify, write, or queue.
   store_query32<APPLY>(a, i, active, qx, qy, qz);
   bool written = false, to_exact = false, to_lane = false;
@@ -1496,6 +1518,7 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
   const bool covered = !(join && !(best <= u));
   wave_append_u(to_lane, i, (WIDE && wide_lane) ? gw : covered ? u : __builtin_inf(), a.fb_count + 1, a.fb_list2,
                 a.fb_u2);
+  PSTOP(6);
   if (!kSecond)
     wave_record<DBG>(a, wid, lane, active, safe || written, safe ? __builtin_sqrt(u) : d, safe ? prev_pos : pos, qx,
                      qy, qz, wl);
@@ -2318,3 +2341,9 @@ hipError_t launch_nn(const NNLaunch& a, hipStream_t s) {
 }
 
 }  // namespace icp
+
+#if ICP_PHASE_STOP
+extern "C" int icp_hip_debug_phase_stop(int k) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(icp::g_phase_stop), &k, sizeof k) == hipSuccess ? 0 : -1;
+}
+#endif
