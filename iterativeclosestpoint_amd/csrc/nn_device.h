@@ -185,6 +185,10 @@ __device__ __forceinline__ int row_incl_scan(int v, int row_base, int* total) {
   *total = __shfl(v, row_base + 15, kWave);
   return v;
 }
+// The wave's ballot of a condition, taken on the condition itself: HIP's wballot(int) first
+// materialises the bool in a vector register (v_cndmask) and compares it again (v_cmp), two VALU
+// instructions per ballot that the compare's own lane mask makes unnecessary.
+__device__ __forceinline__ unsigned long long wballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
 // Position of this lane among the set lanes of a ballot mask.
 __device__ __forceinline__ int mask_rank(unsigned long long m) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
@@ -577,7 +581,7 @@ __device__ __forceinline__ bool fast_dfs(const NNLaunch& a, double qx, double qy
 // Append the lanes with `want` to a list, one atomic per wave, lane order kept (the lists stay
 // in query order wave by wave, which keeps the follow-up searches coherent). Wave-uniform call.
 __device__ __forceinline__ void wave_append(bool want, int64_t i, unsigned* counter, int32_t* list) {
-  const unsigned long long m = __ballot(want);
+  const unsigned long long m = wballot(want);
   if (m == 0) return;
   const int lane = threadIdx.x & 63;
   const int leader = __builtin_ctzll(m);
@@ -590,7 +594,7 @@ __device__ __forceinline__ void wave_append(bool want, int64_t i, unsigned* coun
 // wave_append that also stores a per-entry payload (the guess u of the ball search).
 __device__ __forceinline__ void wave_append_u(bool want, int64_t i, double u, unsigned* counter, int32_t* list,
                                               double* payload) {
-  const unsigned long long m = __ballot(want);
+  const unsigned long long m = wballot(want);
   if (m == 0) return;
   const int lane = threadIdx.x & 63;
   const int leader = __builtin_ctzll(m);
@@ -696,11 +700,11 @@ __device__ __forceinline__ int cell_starts(const NNLaunch& a, double blx, double
       put = cx[k] == fx && cy[k] == fy && cz[k] == fz;
     }
     if (G == 64) {
-      const unsigned long long pm = __ballot(put);
+      const unsigned long long pm = wballot(put);
       if (put) out[count + mask_rank(pm)] = node;
       count += __popcll(pm);
     } else {
-      const uint32_t pm = (uint32_t)((__ballot(put) >> gbase) & ((1ull << G) - 1ull));
+      const uint32_t pm = (uint32_t)((wballot(put) >> gbase) & ((1ull << G) - 1ull));
       if (put) out[count + __builtin_popcount(pm & ((1u << gl) - 1u))] = node;
       count += __builtin_popcount(pm);
     }

@@ -230,7 +230,7 @@ __device__ __forceinline__ void wave_record(const NNLaunch& a, uint32_t wid, int
                                             unsigned char* wl) {
   if (a.wstat == nullptr || !(a.fz->fz_ok != 0.0)) return;
   WaveStat* rec = a.wstat + wid;
-  if (__ballot(active && !settled) != 0) {
+  if (wballot(active && !settled) != 0) {
     if (lane == 0) {
       rec->flag = 1ull;
       if (DBG && kDbgCounts && a.dbg) atomicAdd(&a.dbg[30], 1ull);
@@ -253,7 +253,7 @@ __device__ __forceinline__ void wave_record(const NNLaunch& a, uint32_t wid, int
   for (int k = 0; k < 6; k++) sh[k] = a.fz->fz_sh[k];
   wave_lds_fence();  // the scan's reads of the staging area are done
   const double r = wave_cov_sums(in, d, qx, qy, qz, mx, my, mz, sh, reinterpret_cast<double*>(wl), lane);
-  const unsigned long long am = __ballot(in), bm = __ballot(band);
+  const unsigned long long am = wballot(in), bm = wballot(band);
   if (lane < 16) rec->s[lane] = r;
   if (lane == 0) {
     rec->cnt = (double)__popcll(am);
@@ -464,9 +464,9 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
   //   3: certified lanes settle; a wave left with at most kOpenToBall open queries sends them to
   //      the ball search (with u as their guess) and ends here, otherwise it searches them (2)
   if (CERT && have_prev) {
-    const unsigned long long open = __ballot(active && !safe);
+    const unsigned long long open = wballot(active && !safe);
     if (kDbg && a.dbg) {
-      const unsigned long long settled = __ballot(safe);  // every lane takes part in the ballot
+      const unsigned long long settled = wballot(safe);  // every lane takes part in the ballot
       if (lane == 0) {
         atomicAdd(&a.dbg[19], (unsigned long long)__popcll(settled));
         if (open == 0) atomicAdd(&a.dbg[18], 1ull);
@@ -503,11 +503,11 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
   // |q| <= 2^100 keeps every fp32 offset of the wave finite
   const bool cand = active && finite_q && !safe && u <= 0x1p900 && amax <= 0x1p100;
   float r = cand ? ball_radius32(u, amax) : 0.f;  // (the wide pass shrinks it as its bounds tighten)
-  const unsigned long long cmask = __ballot(cand);
+  const unsigned long long cmask = wballot(cand);
   // the join rule is a heuristic (any subset may join): fp32 mean
   const float mean_r = wave_sum_f(r) * __builtin_amdgcn_rcpf((float)(cmask ? __popcll(cmask) : 1));
   bool join = cand && r <= (float)a.join_factor * mean_r;
-  const unsigned long long jm = __ballot(join);
+  const unsigned long long jm = wballot(join);
 
   // The frame of the box reductions: fp32 offsets from an origin o. A wave whose cache record is of
   // this generation takes o = the centre of its stored B+, the frame its entries were stored in: a
@@ -755,7 +755,7 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
       const uint32_t meta = live ? (uint32_t)topo.y : 0u;
       const uint32_t kids = (live && !(meta & kLeafBit)) ? children_in_box(nd, meta & 0xffu, wlx, wly, wlz, whx, why, whz) : 0u;
       const int lcnt = (live && (meta & kLeafBit)) ? (int)(meta & ~kLeafBit) : 0;
-      if (__ballot(lcnt > kWaveCandCap) != 0) return false;
+      if (wballot(lcnt > kWaveCandCap) != 0) return false;
       int ltot;
       const int lincl = wave_incl_scan(lcnt, &ltot);
       const bool fit = lcnt > 0 && nleaf + lincl <= kWaveCandCap;
@@ -763,7 +763,7 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
       if (fit)
         for (int c = 0; c < lcnt; c++) plist[nleaf + lincl - lcnt + c] = first + c;
       // the points appended: the exclusive sum at the first leaf lane that did not fit
-      const unsigned long long bm = __ballot(back);
+      const unsigned long long bm = wballot(back);
       const int app = bm ? __builtin_amdgcn_readlane(lincl - lcnt, __builtin_ctzll(bm)) : ltot;
       nleaf += app;
       listed += app;
@@ -980,7 +980,7 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
     if (!kSecond && lane == 0) atomicAdd(a.fb_count + 6, 1u);  // the iteration record's n_wide
     if (!HALF && CM != 1 && a.fb_list3 != nullptr) {  // the half pass: first iterates only
       // entries (half id, mask of its deferred lanes): the half pass searches exactly these
-      const unsigned long long dm = __ballot(join);
+      const unsigned long long dm = wballot(join);
       deferred = join;
       const unsigned nh = ((uint32_t)dm != 0u ? 1u : 0u) + ((dm >> 32) != 0ull ? 1u : 0u);
       if (lane == 0 && nh > 0) {
@@ -999,7 +999,7 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
     } else if (!WIDE && a.fb_list4 != nullptr) {
       // the wide pass (k_nn_wide) searches the joined lanes again with the same box, walked and
       // scanned in segments: (first query of the wave or half, lane mask) per entry
-      const unsigned long long dm = __ballot(join);
+      const unsigned long long dm = wballot(join);
       deferred = join;
       if (dm != 0) {
         const int fl = __builtin_ctzll(dm);
@@ -1042,7 +1042,7 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
         if (nb + lane < nleaf) nxtp = load_cand(a.pts, plist[nb + lane]);
         const bool inp = base + lane < nleaf && cur.x >= wlx && cur.x <= whx && cur.y >= wly && cur.y <= why &&
                          cur.z >= wlz && cur.z <= whz && __double_as_longlong(cur.w) >= 0;
-        const unsigned long long pm = __ballot(inp);
+        const unsigned long long pm = wballot(inp);
         if (inp)
           wents[wcount + mask_rank(pm)] = make_float4((float)(cur.x - ocx), (float)(cur.y - ocy), (float)(cur.z - ocz),
                                                       __int_as_float((int)__double_as_longlong(cur.w)));
@@ -1060,7 +1060,7 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
   }
   const int npts = nleaf;
   int scanned_pts = 0;
-  bool need64 = __ballot(join) != 0 && (WIDE || npts > 0);
+  bool need64 = wballot(join) != 0 && (WIDE || npts > 0);
   // the wide pass: lanes it leaves undecided (no certificate, or a walk that overflowed) take the
   // ball search with the tightest upper bound it found (gw: the fp64 fl(d2) of a scanned point)
   bool wide_lane = false;
@@ -1120,6 +1120,15 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
                                          (uint32_t)__builtin_amdgcn_readfirstlane((int)(sl + 1u)));  // a scalar operand
         sel2(ka, kb);
       };
+      // the same for the streamed scan's planes: an axis of the two points per 8-B read
+      auto evalp = [&](const f2 X, const f2 Y, const f2 Z, uint32_t sl) {
+        const f2 dx = X - qx2, dy = Y - qy2, dz = Z - qz2;
+        const f2 sq = __builtin_elementwise_fma(dz, dz, __builtin_elementwise_fma(dy, dy, dx * dx));
+        const float ka = __uint_as_float((__float_as_uint(sq.x) & kmask) | sl);
+        const float kb = __uint_as_float((__float_as_uint(sq.y) & kmask) |
+                                         (uint32_t)__builtin_amdgcn_readfirstlane((int)(sl + 1u)));
+        sel2(ka, kb);
+      };
       const v4i* st4 = reinterpret_cast<const v4i*>(stage32) + 2 * blk(0, gq);  // this group's pair 0
       constexpr int kStep = 2 * NG;                                             // v4i per pair step
       // One chunk of 64 candidates (lane = candidate base + lane; offsets vx, vy, vz, id bits vw):
@@ -1137,7 +1146,7 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
           for (int g = 0; g < NG; g++) {
             const bool in = valid && vx >= gl[g][0] && vx <= gh[g][0] && vy >= gl[g][1] && vy <= gh[g][1] &&
                             vz >= gl[g][2] && vz <= gh[g][2];
-            const unsigned long long mk = __ballot(in);
+            const unsigned long long mk = wballot(in);
             if (count) {
               cn[g] = __popcll(mk);
               maxc = cn[g] > maxc ? cn[g] : maxc;
@@ -1206,9 +1215,22 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
         // lockstep scan then pays max over groups of the wave's whole count once, not of every
         // chunk's count (pairs per wave 34.6 -> ~27 at NG = 4), and fewer rounds. The next
         // chunk's loads are issued before the current one is staged.
+        //
+        // Staged in planes (r23): x, y, z and id each in a plane of its own, a group's segment of
+        // 64 points contiguous in every plane. A point's slot is then one address (the group's
+        // base + the fill, scalar, + 4 x its rank: one v_lshl_add) for its four stores, which land
+        // in the planes at immediate offsets; the scan reads an axis of two points as one 8-B
+        // broadcast (three per pair instead of the pair blocks' 16 + 8 B). The pair blocks cost
+        // five address instructions per staged point. Segments are kGS bytes apart (not 256):
+        // the four groups' reads of one step fall on different banks.
+        constexpr int kPl = 1280;      // bytes per plane: x, y, z, id = the wave's 5 KB
+        constexpr int kGS = kPl / NG;  // a group's segment in a plane
+        static_assert(4 * kPl <= kWaveLds && 64 * 4 <= kGS && kGS % 8 == 0, "planes of the streamed scan");
+        unsigned char* const pl = wl;
         int fill[NG];
 #pragma unroll
         for (int g = 0; g < NG; g++) fill[g] = 0;
+        const unsigned char* const rp = pl + gq * kGS;  // this lane's group segment
         auto scan_round = [&]() {
           int maxf = 0;
 #pragma unroll
@@ -1220,11 +1242,11 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
           for (int g = 1; g < NG; g++) c = pg == g ? fill[g] : c;
           for (int pj = lane % LG; pj < len; pj += LG) {
             if (pj >= c) {
-              float* sp = stage32 + 8 * blk(pj >> 1, pg) + (pj & 1);
-              sp[0] = 0x1p62f;
-              sp[2] = 0x1p62f;
-              sp[4] = 0x1p62f;
-              sp[6] = __int_as_float(-1);
+              unsigned char* q = pl + pg * kGS + 4 * pj;
+              *reinterpret_cast<float*>(q) = 0x1p62f;
+              *reinterpret_cast<float*>(q + kPl) = 0x1p62f;
+              *reinterpret_cast<float*>(q + 2 * kPl) = 0x1p62f;
+              *reinterpret_cast<int32_t*>(q + 3 * kPl) = -1;
             }
           }
           wave_lds_fence();
@@ -1236,11 +1258,13 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
             atomicAdd(&a.dbg[11], 1ull);
           }
 #pragma unroll 1
-          for (int k = 0; k < mp; k++) eval2(st4[kStep * k], st4[kStep * k + 1], 2u * k);
-          if (k1 != k1_in) {
-            const uint32_t sl = __float_as_uint(k1) & 63u;
-            p1 = __float_as_int(stage32[8 * blk((int)(sl >> 1), gq) + 6 + (sl & 1u)]);
+          for (int k = 0; k < mp; k++) {
+            const f2 X = *reinterpret_cast<const f2*>(rp + 8 * k);
+            const f2 Y = *reinterpret_cast<const f2*>(rp + kPl + 8 * k);
+            const f2 Z = *reinterpret_cast<const f2*>(rp + 2 * kPl + 8 * k);
+            evalp(X, Y, Z, 2u * k);
           }
+          if (k1 != k1_in) p1 = *reinterpret_cast<const int32_t*>(rp + 3 * kPl + 4 * (__float_as_uint(k1) & 63u));
           wave_lds_fence();  // the round's reads are done before the slots are rewritten
 #pragma unroll
           for (int g = 0; g < NG; g++) fill[g] = 0;
@@ -1250,28 +1274,32 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
           const float vx = nx.x, vy = nx.y, vz = nx.z, vw = nx.w;
           if (base + 64 + lane < npts) nx = wents[base + 64 + lane];
           const bool valid = base + lane < npts;
-          uint32_t mem = 0;  // this lane's point: member of which groups
+          // membership as lane masks (kept in scalar registers: the second pass takes its exec
+          // mask and ranks from them, with no bool materialised in a vector register)
+          bool ing[NG];
+          unsigned long long mk[NG];
           int cn[NG];
           bool over = false;
 #pragma unroll
           for (int g = 0; g < NG; g++) {
-            const bool in = valid && vx >= gl[g][0] && vx <= gh[g][0] && vy >= gl[g][1] && vy <= gh[g][1] &&
-                            vz >= gl[g][2] && vz <= gh[g][2];
-            mem |= in ? 1u << g : 0u;
-            cn[g] = __popcll(__ballot(in));
+            ing[g] = valid && vx >= gl[g][0] && vx <= gh[g][0] && vy >= gl[g][1] && vy <= gh[g][1] &&
+                     vz >= gl[g][2] && vz <= gh[g][2];
+            mk[g] = wballot(ing[g]);
+            cn[g] = __popcll(mk[g]);
             over = over || fill[g] + cn[g] > SP;
           }
           if (over) scan_round();
 #pragma unroll
           for (int g = 0; g < NG; g++) {
-            const bool in = (mem >> g) & 1u;
-            const int j = fill[g] + mask_rank(__ballot(in));
-            if (in) {
-              float* sp = stage32 + 8 * blk(j >> 1, g) + (j & 1);
-              sp[0] = vx;
-              sp[2] = vy;
-              sp[4] = vz;
-              sp[6] = vw;
+            if (ing[g]) {
+              // the slot: fill + rank (mbcnt's accumulator), one shift-add from the scalar base
+              const int j = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mk[g] >> 32),
+                                                           __builtin_amdgcn_mbcnt_lo((uint32_t)mk[g], (uint32_t)fill[g]));
+              unsigned char* q = pl + g * kGS + 4 * j;
+              *reinterpret_cast<float*>(q) = vx;
+              *reinterpret_cast<float*>(q + kPl) = vy;
+              *reinterpret_cast<float*>(q + 2 * kPl) = vz;
+              *reinterpret_cast<float*>(q + 3 * kPl) = vw;
             }
             fill[g] += cn[g];
             scanned_pts += cn[g];
@@ -1293,7 +1321,7 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
           if (wstore) {
             const bool inp = base + lane < np && !cp && nxtp.x >= wlx && nxtp.x <= whx && nxtp.y >= wly &&
                              nxtp.y <= why && nxtp.z >= wlz && nxtp.z <= whz;
-            const unsigned long long pm = __ballot(inp);
+            const unsigned long long pm = wballot(inp);
             if (inp) wents[wcount + mask_rank(pm)] = make_float4(vx, vy, vz, vw);
             wcount += __popcll(pm);
           }
@@ -1360,7 +1388,7 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
         if (join && p1 >= 0 && b64 < gw) gw = b64;
         wide_lane = join && !dec;
         if (kDbg && a.dbg) {
-          const unsigned long long um = __ballot(wide_lane);
+          const unsigned long long um = wballot(wide_lane);
           if (lane == 0) atomicAdd(&a.dbg[35], (unsigned long long)__popcll(um));
         }
         best = dec ? b64 : __builtin_inf();
@@ -1369,7 +1397,7 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
         need64 = false;
       }
       const bool ok = !join || p1 < 0 || (!(b64 <= u) && lb2 > u) || (b64 <= u && certified(b64, lb2, a.init_best));
-      if (!WIDE && __ballot(!ok) == 0) {
+      if (!WIDE && wballot(!ok) == 0) {
         best = b64;
         second = lb2;
         bpos = p1;
@@ -1415,13 +1443,13 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
     for (int base = 0; base < npts; base += 64) {
       nin = base + lane < npts && nxtp.x >= xlx && nxtp.x <= xhx && nxtp.y >= xly && nxtp.y <= xhy &&
             nxtp.z >= xlz && nxtp.z <= xhz;
-      const unsigned long long im = __ballot(nin);
+      const unsigned long long im = wballot(nin);
       const int slot = mask_rank(im);
       const double4 cur = nxtp;
       if (wstore) {
         const bool inp = base + lane < npts && cur.x >= wlx && cur.x <= whx && cur.y >= wly && cur.y <= why &&
                          cur.z >= wlz && cur.z <= whz;
-        const unsigned long long pm = __ballot(inp);
+        const unsigned long long pm = wballot(inp);
         if (inp)
           wents[wcount + mask_rank(pm)] = make_float4((float)(cur.x - ocx), (float)(cur.y - ocy), (float)(cur.z - ocz),
                                                       __int_as_float((int)__double_as_longlong(cur.w)));
@@ -1471,9 +1499,9 @@ __device__ __forceinline__ void wave_search(const NNLaunch& a, const int32_t i, 
     if (kDbg && a.dbg && lane == 0) atomicAdd(&a.dbg[4], (unsigned long long)scanned_pts);
   }
   if (kDbg && a.dbg) {
-    const unsigned long long ex = __ballot(cand && !join && !overflow);
-    const unsigned long long cov = __ballot(join && !(best <= u));
-    const unsigned long long nc = __ballot(active && finite_q && !safe && !cand);
+    const unsigned long long ex = wballot(cand && !join && !overflow);
+    const unsigned long long cov = wballot(join && !(best <= u));
+    const unsigned long long nc = wballot(active && finite_q && !safe && !cand);
     if (lane == 0) {
       atomicAdd(&a.dbg[2], (unsigned long long)__popcll(ex));
       atomicAdd(&a.dbg[3], (unsigned long long)__popcll(cov));
@@ -1818,7 +1846,7 @@ __device__ __forceinline__ int wave_bb(const NNLaunch& a, int64_t i, double u, i
   // the wave's best, and its second: the smallest of the other lanes' bests and the best lane's
   // second (a best held by two lanes is its own second: a tie)
   const double gb = wave_min_d(best);
-  const unsigned long long at = __ballot(best == gb);
+  const unsigned long long at = wballot(best == gb);
   const double gs = __popcll(at) > 1 ? gb : wave_min_d(best == gb ? second : best);
   const int32_t gp = (int32_t)__builtin_amdgcn_readlane(bpos, __builtin_ctzll(at ? at : 1ull));
   if (!certified(gb, gs, a.init_best)) return 2;
@@ -1870,9 +1898,9 @@ __global__ void __launch_bounds__(64) k_nn_ball(NNLaunch a) {
       qu = found < qu ? found : qu;
     }
     wave_lds_fence();
-    const unsigned long long handed_m = __ballot(handed);
+    const unsigned long long handed_m = wballot(handed);
     if (a.dbg && lane == 0) atomicAdd(&a.dbg[29], (unsigned long long)__popcll(handed_m));
-    for (unsigned long long hm = __ballot(handed); hm; hm &= hm - 1) {
+    for (unsigned long long hm = wballot(handed); hm; hm &= hm - 1) {
       const int k = __builtin_ctzll(hm);
       const int64_t iq = __builtin_amdgcn_readlane(e, k) & 0x3fffffff;
       const double uq = readlane_d(qu, k);
@@ -1967,7 +1995,7 @@ __global__ void __launch_bounds__(64) k_nn_ball(NNLaunch a) {
     }
     wave_lds_fence();
     // LIFO batches of up to 16 nodes per group, sphere test s <= thr on the children
-    while (__ballot(tail > 0) != 0) {
+    while (wballot(tail > 0) != 0) {
       const int batch = tail < kBallGL ? tail : kBallGL;
       const bool has = gl < batch;
       bool leaf = false;
@@ -2061,7 +2089,7 @@ __global__ void __launch_bounds__(64) k_nn_ball(NNLaunch a) {
     }
     // queue the follow-ups (one entry per group: its leader lane)
     const bool fol = follow != 0 && gl == 0;
-    const unsigned long long fm = __ballot(fol);
+    const unsigned long long fm = wballot(fol);
     if (fol) {
       atomicAdd(a.fb_count + (follow == 1 ? 2 : 3), 1u);  // counted for the iteration record
       fq[qn + mask_rank(fm)] = (int32_t)i | (follow << 30);

@@ -93,7 +93,7 @@ __device__ __forceinline__ double wave_cov_sums(bool in, double d, double qx, do
   double da0 = qx - sh[0], da1 = qy - sh[1], da2 = qz - sh[2];
   double db0 = mx - sh[3], db1 = my - sh[4], db2 = mz - sh[5];
   double dd = d * d;
-  if (__ballot(in) != ~0ull) {  // some lane does not count: zero its terms (most waves skip this)
+  if (wballot(in) != ~0ull) {  // some lane does not count: zero its terms (most waves skip this)
     da0 = in ? da0 : 0.0, da1 = in ? da1 : 0.0, da2 = in ? da2 : 0.0;
     db0 = in ? db0 : 0.0, db1 = in ? db1 : 0.0, db2 = in ? db2 : 0.0;
     dd = in ? dd : 0.0;
