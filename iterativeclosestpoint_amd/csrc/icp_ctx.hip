@@ -198,7 +198,7 @@ void icp_hip_config_default(icp_hip_config* cfg) {
   cfg->scan_groups = 4;
   cfg->candidate_cache = 1;
   cfg->candidate_margin = 16;
-  cfg->candidate_loose = 190;
+  cfg->candidate_loose = 1500;
   cfg->candidate_lead = 8;
   cfg->fused_cull = 1;
   cfg->overflow_halves = 0;
@@ -237,7 +237,7 @@ int icp_hip_create_ex(icp_hip_ctx** out, int device, const icp_hip_config* cfg) 
   if (conf.candidate_cache != 0 && conf.candidate_cache != 1) return fail(ICP_HIP_EINVAL, "config: candidate_cache must be 0 or 1");
   if (conf.candidate_margin < 0 || conf.candidate_margin > 1024)
     return fail(ICP_HIP_EINVAL, "config: candidate_margin out of [0, 1024]");
-  if (conf.candidate_loose == 0) conf.candidate_loose = 190;
+  if (conf.candidate_loose == 0) conf.candidate_loose = 1500;
   if (conf.candidate_loose < 100 || conf.candidate_loose > 100000)
     return fail(ICP_HIP_EINVAL, "config: candidate_loose out of [100, 100000]");
   if (conf.candidate_lead < 0 || conf.candidate_lead > 64) return fail(ICP_HIP_EINVAL, "config: candidate_lead out of [0, 64]");

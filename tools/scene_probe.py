@@ -43,7 +43,8 @@ with icp.Context(0, icp.config(**base)) as ctx:
         for k in ("waves", "overflow_waves", "not_joined", "not_covered", "ball_overflow", "ball_points",
                   "fp64_scan_waves", "cache_hits", "scan_pairs", "staged_points", "bb_queries", "bb_steps",
                   "lane_handed", "bb_overflow", "wide_waves", "wide_segments", "wide_stack", "wide_undecided",
-                  "wide_points", "lane_exact"):
+                  "wide_points", "lane_exact", "cache_stores", "walk_moved", "walk_loose", "reused_entries",
+                  "candidates", "group_points"):
             out[k] = c.get(k)
         print(json.dumps(out), flush=True)
     sess.finish()
