@@ -1920,15 +1920,16 @@ __global__ void __launch_bounds__(64) k_nn_ball(NNLaunch a) {
   const unsigned cnt = a.fb_count[1];
   // Direct mode: each wave takes whole queries, one after the other, with all its lanes: the
   // cooperative search started from the cell tables of the query's bound (a few 64-node steps
-  // instead of the 16-lane ball walk and the follow-ups after it). Used for a short list (at most
-  // one query per wave of the launch: the steady state of a dense cloud, ~7.5k of 10M) and for a
-  // long one (over four per wave: an unconverged registration on surface data, where most balls
-  // overflow); the four-queries-per-wave ball walk keeps the lists in between, whose queries are
-  // mostly easy. Measured (profiles/r21/ab_ball_direct.txt): scene 10M 678 -> 1215 Mcorr/s,
+  // instead of the 16-lane ball walk and the follow-ups after it). Used for a long list (over four
+  // per wave: an unconverged registration on surface data, where most balls overflow) and after
+  // the wide pass; the four-queries-per-wave ball walk takes the shorter lists, whose queries are
+  // mostly easy. (Short lists, at most one query per wave, went to the direct mode too until r23:
+  // since the flat leaf scans of r22 the ball walk settles them faster, config 3 6.2k -> 7.4k,
+  // config 2 1.35k -> 1.41k Mcorr/s, profiles/r23/ab_ball_mode_configs23.txt.) Measured (profiles/r21/ab_ball_direct.txt): scene 10M 678 -> 1215 Mcorr/s,
   // scene 1M 624 -> 1254 (driver window), config 4 unchanged; direct at every size cost config
   // 4's window 4 % (its 15k-query lists of easy balls).
   // (icp_hip_config.ball_mode: 0 this rule, 1 the ball walk always, 2 direct always)
-  if (a.ball_mode == 2 || (a.ball_mode == 0 && (cnt <= gridDim.x || cnt > 4u * gridDim.x))) {
+  if (a.ball_mode == 2 || (a.ball_mode == 0 && cnt > 4u * gridDim.x)) {
     // A query the cooperative search leaves (a tie, an overflow) is queued for the reference-order
     // DFS; the queue runs 64 at a time, one per lane, each with its DFS stack column in LDS (ties
     // come in numbers where both clouds sit on the LAS grid: the source's first iterate)
