@@ -587,9 +587,12 @@ __device__ __forceinline__ void add_pair(double* row, double d, double qx, doubl
 // waves per block: 3052 blocks at 50M), at least 8 waves per block (a 100k cloud: 196 blocks;
 // fewer, larger blocks left the small clouds' flagged waves to a handful of waves in sequence:
 // +10 us per iterate at 100k).
+#ifndef ICP_CULL_BLOCKS
+#define ICP_CULL_BLOCKS 600
+#endif
 int cull_waves_per_block(int64_t n) {
   const int64_t nw = (n + 63) / 64;
-  const int64_t w = (nw + 599) / 600;
+  const int64_t w = (nw + ICP_CULL_BLOCKS - 1) / ICP_CULL_BLOCKS;
   return (int)(w < 8 ? 8 : w > kCullWaves ? kCullWaves : w);
 }
 constexpr int kRow = 20;         // doubles per row: the WaveStat layout (s[16], cnt, bm, flag, pad)
